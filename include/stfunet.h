@@ -1,0 +1,194 @@
+/*
+ * stfunet.h -- C ABI of the MI355X (gfx950) STF-Unet training hot path.
+ *
+ * The reference (XiangFeng-Wen/STF-Unet) has no FFI: its hot path is the
+ * PyTorch nn.Module surface of src/unet.py and src/stf_lstm_unet.py plus the
+ * engine functions of train_utils/.  Every entry point below replaces the
+ * PyTorch/MIOpen kernels behind one op *call site* of that path (cited per
+ * function).  The Python host mirror (stf-unet_amd/stfunet) binds them with
+ * ctypes; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Activations: NHWC bf16.  A tensor argument is (pointer to its first used
+ *    channel, channel stride in elements) so producers can write straight into
+ *    a channel slice of a concat buffer ("virtual concat").
+ *  - Weights: bf16, K-contiguous GEMM rows [Nout][R][S][Cs].
+ *  - Statistics, master weights, gradients, optimizer state: fp32.
+ *  - Every function is stream-ordered on `stream` (a hipStream_t), allocates
+ *    nothing, keeps no pointer after it returns and has no mutable global state.
+ *  - Return value: 0 on success, a hipError_t code on launch failure, or
+ *    STF_EINVAL (100001) when the arguments violate a documented constraint.
+ */
+#ifndef STFUNET_H
+#define STFUNET_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* stf_stream_t; /* hipStream_t */
+
+/* Geometry of one implicit-GEMM pass.  GEMM rows m = (n, yd, xd) walk the
+ * destination grid [N][Hd][Wd]; the reduction k = (r, s, c) gathers the source
+ * tensor [N][Hs][Ws][Cs]:
+ *   transposed == 0 : ys = yd*stride - pad + r        (Conv2d forward, ConvT dgrad)
+ *   transposed == 1 : ys = (yd + pad - r) / stride    (Conv2d dgrad, ConvTranspose2d
+ *                     forward); taps with a non-zero remainder contribute 0.
+ */
+typedef struct stf_conv_geom {
+  int N;
+  int Hs, Ws, Cs;      /* source spatial dims and reduction channels            */
+  int src_cstride;     /* elements between consecutive source pixels (>= Cs)   */
+  int Hd, Wd;          /* destination (GEMM row) spatial dims                   */
+  int R, S;            /* taps                                                  */
+  int stride, pad;     /* transposed==1 requires stride in {1, 2}               */
+  int transposed;
+} stf_conv_geom;
+
+typedef struct stf_igemm_args {
+  stf_conv_geom g;
+  const void* src;     /* bf16, first used channel                              */
+  const void* wgt;     /* bf16 [Nout][R*S*Cs]                                   */
+  int Nout;            /* GEMM columns; multiple of 8                           */
+  void* dst;           /* bf16, first channel of the destination slice          */
+  int dst_cstride;
+  const float* bias;   /* [Nout] (scatter2x2: [Nout/4]) or NULL                 */
+  float* stats;        /* [mtiles][2][Nout] per-tile (sum, sum of squares) of   */
+                       /* the stored bf16 outputs, or NULL                      */
+  int scatter2x2;      /* 1: ConvTranspose2d(k=2,s=2) epilogue: column          */
+                       /* n = (dy*2+dx)*Cout + co lands on pixel (2yd+dy,2xd+dx)*/
+                       /* of a [N][2Hd][2Wd] destination                        */
+} stf_igemm_args;
+
+/* Rows per M tile chosen for these args (size `stats` as ceil(M/rows)). */
+int stf_igemm_mtile(const stf_igemm_args* a);
+/* Conv2d 3x3/1x1/strided forward with fused bias + BatchNorm partial statistics
+ *   replaces nn.Conv2d in conv_block  (src/unet.py:12,15), ResidualConvBlock
+ *   (src/stf_lstm_unet.py:13,16,23), ResNet-34 convs (src/stf_lstm_unet.py:108-114),
+ *   out_conv/fusion/pk_fusion 1x1 (src/unet.py:37, src/stf_lstm_unet.py:46,118-121);
+ * Conv2d input gradient (transposed gather) for the same layers;
+ * ConvTranspose2d(k=2,s=2) forward with scatter epilogue straight into the
+ *   concat buffer  (src/unet.py:28-34,47-54) and its input gradient (stride-2 2x2 gather);
+ * ConvTranspose2d(k=3,s=2,p=1,op=1) forward (src/stf_lstm_unet.py:43,135). */
+int stf_igemm(const stf_igemm_args* a, stf_stream_t stream);
+
+typedef struct stf_wgrad_args {
+  stf_conv_geom g;     /* forward geometry; transposed must be 0                */
+  const void* dy;      /* bf16 [N*Hd*Wd][dy_cstride], first used channel        */
+  int dy_cstride;
+  int Nout;            /* columns of dy used; multiple of 8                     */
+  const void* x;       /* bf16 source (gathered as in stf_conv_geom)            */
+  float* ws;           /* workspace [splits][Nout][R*S*Cs] fp32                 */
+  int splits;          /* pixel splits (from stf_wgrad_plan)                    */
+} stf_wgrad_args;
+
+/* Choose splits and report workspace bytes for a weight-gradient pass. */
+int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_bytes);
+/* dW[n][r][s][c] partials = sum over pixels dy[m][n] * x[gather(m,r,s)][c]
+ *   replaces the weight gradient of every Conv2d/ConvTranspose2d above. */
+int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream);
+/* Sum `splits` slabs into out[Nout][Cs][R][S] (PyTorch Conv2d weight layout;
+ * for ConvTranspose2d pass Nout=Cin, Cs=Cout and get [Cin][Cout][R][S]). */
+int stf_wgrad_reduce(const float* ws, int splits, int Nout, int R, int S, int Cs,
+                     float* out, stf_stream_t stream);
+
+/* Per-channel column sums of a bf16 NHWC tensor (bias gradients of ConvT /
+ * 1x1 convs, src/unet.py:28-37).  partial: [ceil(M/256)][C] scratch. */
+int stf_channel_sum(const void* x, int x_cstride, int M, int C, float* partial,
+                    float* out, stf_stream_t stream);
+
+/* ---------------------------------------------------------------- BatchNorm2d
+ * Training-mode BatchNorm2d + ReLU (src/unet.py:13-17; src/stf_lstm_unet.py:14-17,
+ * ResNet bn1/bn2/downsample.1): batch mean, biased variance for normalisation,
+ * unbiased variance into running_var, momentum 0.1, eps 1e-5 (torch defaults).
+ * stats == NULL selects eval mode (normalise with running_mean/var, no update). */
+int stf_bn_finalize(const float* stats, int tiles, int C, int M, const float* gamma,
+                    const float* beta, float momentum, float eps, float* running_mean,
+                    float* running_var, float* mean, float* invstd, float* scale,
+                    float* shift, stf_stream_t stream);
+/* out = relu?(y*scale + shift) into a channel slice; optional fused 2x2 max
+ * pool (MaxPool2d(2), src/unet.py:25,41-45) into `pooled` [N][H/2][W/2][C]. */
+int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int C,
+               const float* scale, const float* shift, int relu, void* out,
+               int out_cstride, void* pooled, stf_stream_t stream);
+/* Backward of BN(+ReLU)(+2x2 max pool):  da = dz + maxpool_bwd(dpool)
+ * (either may be NULL), g = relu ? da * (y*scale+shift > 0) : da, written to
+ * g_out [M][C]; partial[tile][2][C] = (sum g, sum g*xhat).  Returns tiles via
+ * stf_bn_bwd_tiles. */
+int stf_bn_bwd_tiles(int N, int H, int W, int C, int pooled);
+int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const void* y,
+                      int y_cstride, int N, int H, int W, int C, const float* scale,
+                      const float* shift, const float* mean, const float* invstd,
+                      int relu, void* g_out, float* partial, stf_stream_t stream);
+/* dgamma, dbeta and the per-channel coefficients of dy = A*g + B*y + C. */
+int stf_bn_bwd_finalize(const float* partial, int tiles, int C, int M, const float* gamma,
+                        const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                        float* coef, stf_stream_t stream);
+/* dy = A*g + B*y + C (bf16 [M][C]); optional per-tile column sums of dy for
+ * the bias of the preceding conv (bias_partial [ceil(M/256)][C]) reduced to
+ * dbias. */
+int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int M, int C,
+                     const float* coef, void* dy, float* bias_partial, float* dbias,
+                     stf_stream_t stream);
+
+/* ---------------------------------------------------------------- head + loss
+ * UNet OutConv fused with the last BN+ReLU (src/unet.py:16-17,37,56):
+ * logits[b][k][h][w] (fp32 NCHW, the {"out": ...} tensor) =
+ * bias[k] + sum_c relu(y*scale+shift)[c] * W[k][c]. */
+int stf_head_fwd(const void* y, int N, int H, int W, int C, const float* scale,
+                 const float* shift, const float* w, const float* bias, int classes,
+                 float* logits, stf_stream_t stream);
+/* Backward of the head and the BN+ReLU it absorbed: g = (dlogits . W) * relu',
+ * partial (sum g, sum g*xhat) as stf_bn_bwd_reduce, head dW/db partials in
+ * head_partial [(tiles+1)][classes*(C+1)] (last row = the reduction) copied
+ * into dw (classes*C) and db (classes).  tiles = stf_head_tiles(N, H, W, C). */
+int stf_head_bwd(const float* dlogits, const void* y, int N, int H, int W, int C,
+                 const float* scale, const float* shift, const float* mean,
+                 const float* invstd, const float* w, int classes, void* g_out,
+                 float* bn_partial, float* head_partial, float* dw, float* db,
+                 stf_stream_t stream);
+int stf_head_tiles(int N, int H, int W, int C);
+
+/* criterion (train_utils/train_and_eval.py:299-313) = cross_entropy +
+ * multiclass Dice loss on softmax (train_utils/dice_coefficient_loss.py:5-55),
+ * branch-free empty-set rule.  terms: stf_loss_scratch_floats() floats; its
+ * first N*classes*3 + 1 hold (sum p*t, sum p, sum t) per (image, class) and the
+ * CE sum after stf_loss_fwd; loss: device scalar. */
+int stf_loss_scratch_floats(int N, int classes);
+int stf_loss_fwd(const float* logits, const int64_t* target, int N, int H, int W,
+                 int classes, float* terms, float* loss, stf_stream_t stream);
+int stf_loss_bwd(const float* logits, const int64_t* target, int N, int H, int W,
+                 int classes, const float* terms, const float* grad_out, float* dlogits,
+                 stf_stream_t stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.AdamW(lr, betas, eps, weight_decay) (train.py:230-237) over one
+ * flat fp32 parameter buffer. */
+int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+              float beta1, float beta2, float eps, float weight_decay, float bc1,
+              float bc2, stf_stream_t stream);
+
+/* ---------------------------------------------------------------- layout
+ * x [N][C][H][W] fp32 -> NHWC bf16 with Cpad (>= C, multiple of 8) channels,
+ * zero-filled (preprocess_input output, train_and_eval.py:9-22). */
+int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* out,
+                   stf_stream_t stream);
+/* fp32 weights -> bf16 GEMM rows.
+ *  mode 0: Conv2d w[Co][Ci][R][S]       -> [Co][R][S][Cipad]   (forward)
+ *  mode 1: Conv2d w[Co][Ci][R][S]       -> [Ci][R'][S'][Co]    (dgrad, no flip:
+ *          the transposed gather indexes taps directly)
+ *  mode 2: ConvT  w[Ci][Co][R][S]       -> [(r*S+s)*Co+co][Ci] (scatter2x2 fwd)
+ *  mode 3: ConvT  w[Ci][Co][R][S]       -> [Ci][R][S][Co]      (ConvT dgrad)
+ *  mode 4: ConvT  w[Ci][Co][R][S]       -> [Co][R][S][Ci]      (ConvT fwd gather) */
+int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad,
+                    void* out, stf_stream_t stream);
+
+const char* stf_error_string(int code);
+int stf_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STFUNET_H */

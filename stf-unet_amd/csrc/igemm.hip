@@ -1,0 +1,268 @@
+// Implicit-GEMM convolution on MFMA (gfx950): forward / dgrad / transposed-conv.
+//
+// GEMM view: D[n][m] = sum_k W[n][k] * X[m][k]
+//   m = destination pixel (N*Hd*Wd rows), n = output channel, k = (r, s, c) over
+//   the gathered source tensor (stf_conv_geom in include/stfunet.h).
+// The weight tile is the MFMA A operand and the im2col tile the B operand, so
+// each lane ends with 4 consecutive *channels* of one pixel: the epilogue packs
+// them into one 8-byte store (NHWC), adds bias, and reduces per-channel BatchNorm
+// partial sums (sum, sum^2 of the bf16-rounded values) without another pass.
+//
+// Tiling: 256 threads = 4 waves, BK = 32 (= one v_mfma_f32_16x16x32_bf16 K),
+// register-staged global->LDS double buffer, one barrier per K step.  LDS rows
+// are 64 B; the 16-B chunk of row r is stored at chunk ^ ((-(r>>2)) & 3), which
+// makes the ds_read_b128 fragment reads conflict-free for all four lane groups.
+#include "common.h"
+#include "../../include/stfunet.h"
+
+namespace {
+
+constexpr int BK = 32;
+constexpr int NT = 256;
+
+struct Geo {
+  const uint16_t* src; const uint16_t* wgt; uint16_t* dst;
+  const float* bias; float* stats;
+  int N, Hs, Ws, Cs, scs, Hd, Wd, R, S, st, pad, M, K, Nout, dcs;
+};
+
+STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
+
+template <int BM, int BN, int WM, int WN, bool SMALLC, bool TRANS, bool SCATTER>
+__global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;     // wave tile (pixels x channels)
+  constexpr int TM = WTM / 16, TN = WTN / 16;     // 16x16 fragments per wave
+  constexpr int CHA = BM * BK / 8 / NT;           // 16-B chunks per thread (im2col)
+  constexpr int CHB = BN * BK / 8 / NT;           // 16-B chunks per thread (weights)
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(CHA >= 1 && CHB >= 1, "tile too small");
+  constexpr int LDS_A = BM * BK * 2, LDS_B = BN * BK * 2;
+  constexpr int LDS_MAIN = 2 * (LDS_A + LDS_B), LDS_RED = WM * 2 * BN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kc = tid & 3;                 // this thread's 16-B chunk within a 64-B row
+
+  // per-row gather state for the im2col rows this thread stages
+  int rbase[CHA], ry[CHA], rx[CHA];
+  bool rok[CHA];
+#pragma unroll
+  for (int i = 0; i < CHA; ++i) {
+    const int m = m0 + (tid >> 2) + i * (NT / 4);
+    rok[i] = m < a.M;
+    const int mm = rok[i] ? m : 0;
+    const int hw = a.Hd * a.Wd;
+    const int n = mm / hw, rem = mm - n * hw;
+    const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+    rbase[i] = n * a.Hs * a.Ws;
+    if (TRANS) { ry[i] = yd + a.pad; rx[i] = xd + a.pad; }
+    else { ry[i] = yd * a.st - a.pad; rx[i] = xd * a.st - a.pad; }
+  }
+
+  uint4 ra[CHA], rb[CHB];
+  int tr = 0, ts = 0, tc = 0;             // tap / channel cursor of the next K step (non-SMALLC)
+  const int KT = (a.K + BK - 1) / BK;
+
+  auto gather_src = [&](int i, int r, int s, int c, uint4& out) {
+    int ys, xs; bool ok = rok[i];
+    if (TRANS) {
+      const int ty = ry[i] - r, tx = rx[i] - s;
+      if (a.st == 2) { ok = ok && !(ty & 1) && !(tx & 1); ys = ty >> 1; xs = tx >> 1; }
+      else { ys = ty; xs = tx; }
+      ok = ok && ty >= 0 && tx >= 0;
+    } else { ys = ry[i] + r; xs = rx[i] + s; ok = ok && ys >= 0 && xs >= 0; }
+    ok = ok && ys < a.Hs && xs < a.Ws;
+    out = make_uint4(0, 0, 0, 0);
+    if (ok) out = *reinterpret_cast<const uint4*>(a.src + (size_t)(rbase[i] + ys * a.Ws + xs) * a.scs + c);
+  };
+
+  auto load_tiles = [&](int kt) {
+    const int k0 = kt * BK;
+    if (SMALLC) {
+      const int k = k0 + kc * 8;
+      const bool kok = k < a.K;
+      const int tap = kok ? k / a.Cs : 0;
+      const int c = k - tap * a.Cs;
+      const int r = tap / a.S, s = tap - r * a.S;
+#pragma unroll
+      for (int i = 0; i < CHA; ++i) {
+        if (kok) gather_src(i, r, s, c, ra[i]); else ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CHA; ++i) gather_src(i, tr, ts, tc + kc * 8, ra[i]);
+      tc += BK;
+      if (tc == a.Cs) { tc = 0; if (++ts == a.S) { ts = 0; ++tr; } }
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int n = n0 + (tid >> 2) + i * (NT / 4);
+      const int k = k0 + kc * 8;
+      rb[i] = make_uint4(0, 0, 0, 0);
+      if (n < a.Nout && k < a.K) rb[i] = *reinterpret_cast<const uint4*>(a.wgt + (size_t)n * a.K + k);
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    char* sa = smem + buf * (LDS_A + LDS_B);
+    char* sb = sa + LDS_A;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) {
+      const int row = (tid >> 2) + i * (NT / 4);
+      *reinterpret_cast<uint4*>(sa + row * 64 + swz(row, kc) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int row = (tid >> 2) + i * (NT / 4);
+      *reinterpret_cast<uint4*>(sb + row * 64 + swz(row, kc) * 16) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_tiles(kt + 1);
+    const char* sa = smem + cur * (LDS_A + LDS_B);
+    const char* sb = sa + LDS_A;
+    bf16x8 xf[TM], wf[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + fr;
+      xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * 64 + swz(row, fk) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * WTN + j * 16 + fr;
+      wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * 64 + swz(row, fk) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+    if (kt + 1 < KT) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  // acc[i][j][r]: pixel m = m0 + wm*WTM + i*16 + fr, channel n = n0 + wn*WTN + j*16 + fk*4 + r
+  const int Cout = SCATTER ? a.Nout / 4 : a.Nout;
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nb = n0 + wn * WTN + j * 16 + fk * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && nb < a.Nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = a.bias[SCATTER ? (nb + r) % Cout : nb + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = round_bf(acc[i][j][r] + bv[r]);
+      if (m < a.M && nb < a.Nout) {
+        uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        size_t off;
+        if (SCATTER) {
+          const int blk = nb / Cout, co = nb - blk * Cout;
+          const int hw = a.Hd * a.Wd;
+          const int n = m / hw, rem = m - n * hw;
+          const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+          const int yo = 2 * yd + (blk >> 1), xo = 2 * xd + (blk & 1);
+          off = ((size_t)(n * 2 * a.Hd + yo) * (2 * a.Wd) + xo) * a.dcs + co;
+        } else {
+          off = (size_t)m * a.dcs + nb;
+        }
+        *reinterpret_cast<uint2*>(a.dst + off) = pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
+      }
+    }
+  }
+  if (a.stats == nullptr) return;
+  // reduce over the 16 pixels held by lanes with equal fk, then over the WM waves
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      }
+  float* red = reinterpret_cast<float*>(smem);     // [WM][2][BN]
+  __syncthreads();
+  if (fr == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WTN + j * 16 + fk * 4 + r;
+        red[(wm * 2 + 0) * BN + col] = s1[j][r];
+        red[(wm * 2 + 1) * BN + col] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  for (int col = tid; col < BN; col += NT) {
+    const int n = n0 + col;
+    if (n >= a.Nout) continue;
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { t1 += red[(w * 2) * BN + col]; t2 += red[(w * 2 + 1) * BN + col]; }
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + n] = t1;
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + a.Nout + n] = t2;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, hipStream_t s) {
+  dim3 grid((g.M + BM - 1) / BM, (g.Nout + BN - 1) / BN), block(NT);
+#define STF_L(SC, TR, SCA) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA>), grid, block, 0, s, g)
+  if (scatter) { if (smallc) STF_L(true, false, true); else STF_L(false, false, true); }
+  else if (trans) { if (smallc) STF_L(true, true, false); else STF_L(false, true, false); }
+  else { if (smallc) STF_L(true, false, false); else STF_L(false, false, false); }
+#undef STF_L
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+int pick_mtile(const stf_igemm_args* a) { return a->Nout <= 64 ? 256 : 128; }
+
+}  // namespace
+
+extern "C" int stf_igemm_mtile(const stf_igemm_args* a) { return pick_mtile(a); }
+
+extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
+  const stf_conv_geom& c = a->g;
+  if (a->Nout % 8 || c.Cs % 8 || c.src_cstride % 8 || a->dst_cstride % 4) return STF_EINVAL;
+  if (c.transposed && !(c.stride == 1 || c.stride == 2)) return STF_EINVAL;
+  if (a->scatter2x2 && (c.transposed || (a->Nout / 4) % 4)) return STF_EINVAL;
+  if (((uintptr_t)a->src & 15) || ((uintptr_t)a->wgt & 15) || ((uintptr_t)a->dst & 7)) return STF_EINVAL;
+  Geo g;
+  g.src = (const uint16_t*)a->src; g.wgt = (const uint16_t*)a->wgt; g.dst = (uint16_t*)a->dst;
+  g.bias = a->bias; g.stats = a->stats;
+  g.N = c.N; g.Hs = c.Hs; g.Ws = c.Ws; g.Cs = c.Cs; g.scs = c.src_cstride;
+  g.Hd = c.Hd; g.Wd = c.Wd; g.R = c.R; g.S = c.S; g.st = c.stride; g.pad = c.pad;
+  g.M = c.N * c.Hd * c.Wd; g.K = c.R * c.S * c.Cs; g.Nout = a->Nout; g.dcs = a->dst_cstride;
+  if (g.M <= 0) return 0;
+  const bool smallc = (c.Cs % BK) != 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (pick_mtile(a) == 256) return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, s);
+  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, s);
+}

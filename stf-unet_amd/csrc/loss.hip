@@ -1,0 +1,365 @@
+// Segmentation head (1x1 OutConv fused with the last BN+ReLU) and the
+// CE + multiclass-Dice criterion, forward and backward.
+//
+// Head: a = relu(y*scale + shift) is never materialised -- 8 lanes per pixel
+// each take 8 channels, form partial logits and reduce them with xor shuffles.
+// Loss (train_and_eval.py:299-313, dice_coefficient_loss.py:5-55), per image b
+// and class k with p = softmax(logits), t = one_hot(target):
+//   I = sum p t, S = sum p + sum t, D = (2I + eps)/(S + eps)  (S == 0 -> D = 1),
+//   loss = mean CE + 1 - mean_k mean_b D.
+// Backward: dz = go * [ (p - t)/Npix + p (G - sum_j p_j G_j) ],
+//   G_k = -(1/(K*B)) dD/dp = -(1/(K*B)) (2 t/(S+eps) - (2I+eps)/(S+eps)^2).
+#include "common.h"
+#include "../../include/stfunet.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int MAXK = 4;          // classes supported by the fused kernels
+constexpr int LCHUNK = 64;       // loss partial chunks per image
+constexpr float DICE_EPS = 1e-6f;
+
+STF_DEV void load8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+int head_tiles(long units) {
+  long t = (units + NT - 1) / NT;
+  return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
+}
+
+template <int K>
+__global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, int C,
+                                const float* __restrict__ scale, const float* __restrict__ shift,
+                                const float* __restrict__ w, const float* __restrict__ bias,
+                                float* __restrict__ logits) {
+  const int CG = C / 8;
+  const long units = P * CG;
+  // CG lanes of one pixel are adjacent; loop bound is uniform per CG group
+  for (long u0 = blockIdx.x * (long)NT; u0 < units; u0 += (long)gridDim.x * NT) {
+    const long u = u0 + threadIdx.x;
+    const bool ok = u < units;
+    const int cg = (int)(u % CG);
+    const long pix = u / CG;
+    float acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] = 0.f;
+    if (ok) {
+      float v[8], sc[8], sh[8];
+      unpack8(*reinterpret_cast<const uint4*>(y + pix * C + cg * 8), v);
+      load8f(scale + cg * 8, sc);
+      load8f(shift + cg * 8, sh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sh[j], 0.f);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float wk[8];
+        load8f(w + k * C + cg * 8, wk);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k] += v[j] * wk[j];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      for (int o = 1; o < CG; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+    if (ok && cg == 0) {
+      const long n = pix / HW, hw = pix - n * HW;
+#pragma unroll
+      for (int k = 0; k < K; ++k) logits[(n * K + k) * HW + hw] = acc[k] + bias[k];
+    }
+  }
+}
+
+template <int K>
+__global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_t* __restrict__ y, long P, int HW,
+                                int C, const float* __restrict__ scale, const float* __restrict__ shift,
+                                const float* __restrict__ mean, const float* __restrict__ invstd,
+                                const float* __restrict__ w, uint16_t* __restrict__ g_out,
+                                float* __restrict__ bn_partial, float* __restrict__ head_partial) {
+  constexpr int NV = 16 + 8 * K + K;       // sg[8], sgx[8], dW[K][8], db[K]
+  __shared__ float red[NT][NV + 1];
+  const int CG = C / 8;
+  const long units = P * CG;
+  const long gt = blockIdx.x * (long)NT + threadIdx.x;
+  const int cg = (int)(gt % CG);
+  float sc[8], sh[8], mu[8], is[8], wk[K][8];
+  load8f(scale + cg * 8, sc);
+  load8f(shift + cg * 8, sh);
+  load8f(mean + cg * 8, mu);
+  load8f(invstd + cg * 8, is);
+#pragma unroll
+  for (int k = 0; k < K; ++k) load8f(w + k * C + cg * 8, wk[k]);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dw[K][8], db[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    db[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[k][j] = 0.f;
+  }
+  for (long u = gt; u < units; u += (long)gridDim.x * NT) {
+    const long pix = u / CG;
+    const long n = pix / HW, hw = pix - n * HW;
+    float dl[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dl[k] = dlogits[(n * K + k) * HW + hw];
+    float v[8], g[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + pix * C + cg * 8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float z = v[j] * sc[j] + sh[j];
+      const float a = fmaxf(z, 0.f);
+      float da = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) { da += dl[k] * wk[k][j]; dw[k][j] += dl[k] * a; }
+      g[j] = z > 0.f ? da : 0.f;
+      sg[j] += g[j];
+      sgx[j] += g[j] * (v[j] - mu[j]) * is[j];
+    }
+    if (cg == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) db[k] += dl[k];
+    }
+    *reinterpret_cast<uint4*>(g_out + pix * C + cg * 8) = pack8(g);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][16 + k * 8 + j] = dw[k][j];
+    red[threadIdx.x][16 + 8 * K + k] = db[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int gg = c / 8, j = c - gg * 8;
+    float a = 0.f, b = 0.f;
+    for (int t = gg; t < NT; t += CG) { a += red[t][j]; b += red[t][8 + j]; }
+    bn_partial[(size_t)blockIdx.x * 2 * C + c] = a;
+    bn_partial[(size_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+  const int HC = K * (C + 1);
+  for (int e = threadIdx.x; e < HC; e += NT) {
+    float a = 0.f;
+    if (e < K * C) {
+      const int k = e / C, c = e - k * C, gg = c / 8, j = c - gg * 8;
+      for (int t = gg; t < NT; t += CG) a += red[t][16 + k * 8 + j];
+    } else {
+      const int k = e - K * C;
+      for (int t = 0; t < NT; t += CG) a += red[t][16 + 8 * K + k];
+    }
+    head_partial[(size_t)blockIdx.x * HC + e] = a;
+  }
+}
+
+// ------------------------------------------------------------------ loss
+template <int K>
+__global__ void loss_fwd_kernel(const float* __restrict__ logits, const int64_t* __restrict__ target, int HW,
+                                float* __restrict__ part) {
+  // grid (LCHUNK, N): partial[n][chunk][3K + 1]
+  constexpr int NV = 3 * K + 1;
+  __shared__ float red[NT / 64][NV];
+  const int n = blockIdx.y;
+  float s[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s[i] = 0.f;
+  for (int hw = blockIdx.x * NT + threadIdx.x; hw < HW; hw += gridDim.x * NT) {
+    float z[K], e[K], mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { z[k] = logits[((long)n * K + k) * HW + hw]; mx = fmaxf(mx, z[k]); }
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { e[k] = expf(z[k] - mx); se += e[k]; }
+    const int t = (int)target[(long)n * HW + hw];
+    const float inv = 1.f / se, lse = logf(se);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float p = e[k] * inv;
+      const float tk = t == k ? 1.f : 0.f;
+      s[3 * k] += p * tk;
+      s[3 * k + 1] += p;
+      s[3 * k + 2] += tk;
+      if (t == k) s[3 * K] += lse - (z[k] - mx);   // -log_softmax, stable when p underflows
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s[i] = wave_sum(s[i]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[threadIdx.x >> 6][i] = s[i];
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    float a = 0.f;
+    for (int wv = 0; wv < NT / 64; ++wv) a += red[wv][threadIdx.x];
+    part[((size_t)n * gridDim.x + blockIdx.x) * NV + threadIdx.x] = a;
+  }
+}
+
+template <int K>
+__global__ void loss_finalize_kernel(const float* __restrict__ part, int N, int HW, float* __restrict__ terms,
+                                     float* __restrict__ loss) {
+  constexpr int NV = 3 * K + 1;
+  // one thread per (n, value), fixed summation order over chunks
+  __shared__ double acc[64][NV];
+  double ce = 0.0, dsum = 0.0;
+  for (int base = 0; base < N; base += 64) {
+    const int n = base + (int)threadIdx.x;
+    if (threadIdx.x < 64) {
+      for (int i = 0; i < NV; ++i) {
+        double a = 0.0;
+        if (n < N)
+          for (int c = 0; c < LCHUNK; ++c) a += part[((size_t)n * LCHUNK + c) * NV + i];
+        acc[threadIdx.x][i] = a;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int r = 0; r < 64 && base + r < N; ++r) {
+        for (int k = 0; k < K; ++k) {
+          const double I = acc[r][3 * k], S = acc[r][3 * k + 1] + acc[r][3 * k + 2];
+          const float If = (float)I, Sf = (float)S;
+          const float setsum = Sf == 0.f ? 2.f * If : Sf;
+          dsum += (double)((2.f * If + DICE_EPS) / (setsum + DICE_EPS));
+          terms[((size_t)(base + r) * K + k) * 3 + 0] = If;
+          terms[((size_t)(base + r) * K + k) * 3 + 1] = (float)acc[r][3 * k + 1];
+          terms[((size_t)(base + r) * K + k) * 3 + 2] = (float)acc[r][3 * k + 2];
+        }
+        ce += acc[r][3 * K];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    terms[(size_t)N * K * 3] = (float)ce;
+    loss[0] = (float)(ce / ((double)N * HW) + 1.0 - dsum / ((double)N * K));
+  }
+}
+
+template <int K>
+__global__ void loss_bwd_kernel(const float* __restrict__ logits, const int64_t* __restrict__ target, int N, int HW,
+                                const float* __restrict__ terms, const float* __restrict__ grad_out,
+                                float* __restrict__ dlogits) {
+  const long P = (long)N * HW;
+  const float go = grad_out ? grad_out[0] : 1.f;
+  const float inv_pix = 1.f / (float)P;
+  const float dscale = -1.f / (float)(K * N);
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < P; i += (long)gridDim.x * NT) {
+    const long n = i / HW, hw = i - n * HW;
+    float z[K], mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { z[k] = logits[(n * K + k) * HW + hw]; mx = fmaxf(mx, z[k]); }
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) { z[k] = expf(z[k] - mx); se += z[k]; }
+    const int t = (int)target[i];
+    float p[K], G[K], pg = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      p[k] = z[k] / se;
+      const float I = terms[(n * K + k) * 3], S = terms[(n * K + k) * 3 + 1] + terms[(n * K + k) * 3 + 2];
+      const float tk = t == k ? 1.f : 0.f;
+      float dd = 0.f;
+      if (S != 0.f) {
+        const float den = S + DICE_EPS;
+        dd = 2.f * tk / den - (2.f * I + DICE_EPS) / (den * den);
+      }
+      G[k] = dscale * dd;
+      pg += p[k] * G[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float tk = t == k ? 1.f : 0.f;
+      dlogits[(n * K + k) * HW + hw] = go * ((p[k] - tk) * inv_pix + p[k] * (G[k] - pg));
+    }
+  }
+}
+
+__global__ void sum_tiles_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int t = 0; t < tiles; ++t) s += partial[(size_t)t * C + c];
+  out[c] = (float)s;
+}
+
+bool head_ok(int C) { return C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0; }
+
+}  // namespace
+
+#define STF_KDISPATCH(K_, EXPR)             \
+  switch (K_) {                             \
+    case 1: { constexpr int KK = 1; EXPR; } break; \
+    case 2: { constexpr int KK = 2; EXPR; } break; \
+    case 3: { constexpr int KK = 3; EXPR; } break; \
+    case 4: { constexpr int KK = 4; EXPR; } break; \
+    default: return STF_EINVAL;             \
+  }
+
+extern "C" int stf_head_tiles(int N, int H, int W, int C) { return head_tiles((long)N * H * W * (C / 8)); }
+
+extern "C" int stf_head_fwd(const void* y, int N, int H, int W, int C, const float* scale, const float* shift,
+                            const float* w, const float* bias, int classes, float* logits, stf_stream_t stream) {
+  if (!head_ok(C)) return STF_EINVAL;
+  const long P = (long)N * H * W, units = P * (C / 8);
+  long blocks = (units + NT - 1) / NT;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  STF_KDISPATCH(classes, hipLaunchKernelGGL(head_fwd_kernel<KK>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y,
+                                            P, H * W, C, scale, shift, w, bias, logits));
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_head_bwd(const float* dlogits, const void* y, int N, int H, int W, int C, const float* scale,
+                            const float* shift, const float* mean, const float* invstd, const float* w, int classes,
+                            void* g_out, float* bn_partial, float* head_partial, float* dw, float* db,
+                            stf_stream_t stream) {
+  if (!head_ok(C)) return STF_EINVAL;
+  const long P = (long)N * H * W;
+  const int tiles = stf_head_tiles(N, H, W, C);
+  hipStream_t s = (hipStream_t)stream;
+  STF_KDISPATCH(classes, hipLaunchKernelGGL(head_bwd_kernel<KK>, dim3(tiles), dim3(NT), 0, s, dlogits,
+                                            (const uint16_t*)y, P, H * W, C, scale, shift, mean, invstd, w,
+                                            (uint16_t*)g_out, bn_partial, head_partial));
+  STF_CHECK_LAUNCH();
+  const int HC = classes * (C + 1);
+  // reduce [tiles][K*(C+1)] into row `tiles` of the slab, then split into dw[K*C], db[K]
+  hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, tiles, HC,
+                     head_partial + (size_t)tiles * HC);
+  STF_CHECK_LAUNCH();
+  hipError_t e = hipMemcpyAsync(dw, head_partial + (size_t)tiles * HC, sizeof(float) * classes * C,
+                                hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(db, head_partial + (size_t)tiles * HC + classes * C, sizeof(float) * classes,
+                       hipMemcpyDeviceToDevice, s);
+  return (int)e;
+}
+
+extern "C" int stf_loss_scratch_floats(int N, int classes) {
+  return N * classes * 3 + 1 + N * LCHUNK * (3 * classes + 1);
+}
+
+extern "C" int stf_loss_fwd(const float* logits, const int64_t* target, int N, int H, int W, int classes,
+                            float* terms, float* loss, stf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  float* part = terms + N * classes * 3 + 1;
+  STF_KDISPATCH(classes, {
+    hipLaunchKernelGGL(loss_fwd_kernel<KK>, dim3(LCHUNK, N), dim3(NT), 0, s, logits, target, H * W, part);
+    hipLaunchKernelGGL(loss_finalize_kernel<KK>, dim3(1), dim3(64), 0, s, part, N, H * W, terms, loss);
+  });
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_loss_bwd(const float* logits, const int64_t* target, int N, int H, int W, int classes,
+                            const float* terms, const float* grad_out, float* dlogits, stf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long P = (long)N * H * W;
+  long blocks = (P + NT - 1) / NT;
+  if (blocks > 8192) blocks = 8192;
+  STF_KDISPATCH(classes, hipLaunchKernelGGL(loss_bwd_kernel<KK>, dim3(blocks), dim3(NT), 0, s, logits, target, N,
+                                            H * W, terms, grad_out, dlogits));
+  STF_CHECK_LAUNCH();
+  return 0;
+}

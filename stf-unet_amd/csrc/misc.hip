@@ -1,0 +1,182 @@
+// Flat AdamW, layout packs (input NCHW fp32 -> NHWC bf16, fp32 weights -> bf16
+// GEMM rows), per-channel column sums, and the error-string helper.
+#include "common.h"
+#include "../../include/stfunet.h"
+
+__global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out);
+
+namespace {
+
+constexpr int NT = 256;
+
+// torch.optim.AdamW (decoupled weight decay), PyTorch evaluation order:
+//   p *= 1 - lr*wd;  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;
+//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
+                             float step_size, float inv_sqrt_bc2) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pp = &pv.x; const float* gg = &gv.x; float* mm = &mv.x; float* ww = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pp[j] *= 1.f - lr * wd;
+      mm[j] = mm[j] + (1.f - b1) * (gg[j] - mm[j]);
+      ww[j] = b2 * ww[j] + (1.f - b2) * gg[j] * gg[j];
+      pp[j] -= step_size * mm[j] / (sqrtf(ww[j]) * inv_sqrt_bc2 + eps);
+    }
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(m)[i] = mv;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    float pp = p[i] * (1.f - lr * wd);
+    const float gg = g[i];
+    const float mm = m[i] + (1.f - b1) * (gg - m[i]);
+    const float ww = b2 * v[i] + (1.f - b2) * gg * gg;
+    pp -= step_size * mm / (sqrtf(ww) * inv_sqrt_bc2 + eps);
+    p[i] = pp; m[i] = mm; v[i] = ww;
+  }
+}
+
+__global__ void pack_input_kernel(const float* __restrict__ x, int N, int C, int H, int W, int Cpad,
+                                  uint16_t* __restrict__ out) {
+  const long HW = (long)H * W, P = N * HW;
+  const int CG = Cpad / 8;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < P * CG; u += (long)gridDim.x * NT) {
+    const long pix = u % P;            // consecutive threads -> consecutive pixels (coalesced reads)
+    const int cg = (int)(u / P);
+    const long n = pix / HW, hw = pix - n * HW;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      v[j] = c < C ? x[(n * C + c) * HW + hw] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(out + pix * Cpad + cg * 8) = pack8(v);
+  }
+}
+
+// out element index -> source index, per mode (see include/stfunet.h)
+__global__ void pack_weight_kernel(const float* __restrict__ w, int d0, int d1, int R, int S, int mode, int cpad,
+                                   uint16_t* __restrict__ out) {
+  const int RS = R * S;
+  long total;
+  if (mode == 0) total = (long)d0 * RS * cpad;
+  else total = (long)d0 * d1 * RS;
+  for (long o = blockIdx.x * (long)NT + threadIdx.x; o < total; o += (long)gridDim.x * NT) {
+    float v = 0.f;
+    if (mode == 0) {            // Conv2d w[Co=d0][Ci=d1][R][S] -> [Co][R][S][cpad]
+      const int c = (int)(o % cpad);
+      const long t = o / cpad;
+      const int tap = (int)(t % RS), co = (int)(t / RS);
+      if (c < d1) v = w[((long)co * d1 + c) * RS + tap];
+    } else if (mode == 1) {     // Conv2d -> [Ci][R][S][Co]
+      const int co = (int)(o % d0);
+      const long t = o / d0;
+      const int tap = (int)(t % RS), ci = (int)(t / RS);
+      v = w[((long)co * d1 + ci) * RS + tap];
+    } else if (mode == 2) {     // ConvT w[Ci=d0][Co=d1][R][S] -> [(tap)*Co + co][Ci]
+      const int ci = (int)(o % d0);
+      const long t = o / d0;
+      const int co = (int)(t % d1), tap = (int)(t / d1);
+      v = w[((long)ci * d1 + co) * RS + tap];
+    } else if (mode == 3) {     // ConvT -> [Ci][R][S][Co]
+      const int co = (int)(o % d1);
+      const long t = o / d1;
+      const int tap = (int)(t % RS), ci = (int)(t / RS);
+      v = w[((long)ci * d1 + co) * RS + tap];
+    } else {                    // mode 4: ConvT -> [Co][R][S][Ci]
+      const int ci = (int)(o % d0);
+      const long t = o / d0;
+      const int tap = (int)(t % RS), co = (int)(t / RS);
+      v = w[((long)ci * d1 + co) * RS + tap];
+    }
+    reinterpret_cast<bf16*>(out)[o] = f2bf(v);
+  }
+}
+
+__global__ void channel_sum_kernel(const uint16_t* __restrict__ x, int xcs, long M, int C,
+                                   float* __restrict__ partial) {
+  __shared__ float red[NT][9];
+  const int CG = C / 8;
+  const long gt = blockIdx.x * (long)NT + threadIdx.x;
+  const int cg = (int)(gt % CG);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long u = gt; u < M * CG; u += (long)gridDim.x * NT) {
+    const long pix = u / CG;
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + pix * xcs + cg * 8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = s[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int g = c / 8, j = c - g * 8;
+    float a = 0.f;
+    for (int t = g; t < NT; t += CG) a += red[t][j];
+    partial[(size_t)blockIdx.x * C + c] = a;
+  }
+}
+
+long grid_for(long units, long cap) {
+  long b = (units + NT - 1) / NT;
+  return b < 1 ? 1 : (b > cap ? cap : b);
+}
+
+}  // namespace
+
+extern "C" int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                         float eps, float weight_decay, float bc1, float bc2, stf_stream_t stream) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return STF_EINVAL;
+  const long blocks = grid_for(n / 4 + 1, 4096);
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
+                     beta2, eps, weight_decay, lr / bc1, 1.f / sqrtf(bc2));
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* out, stf_stream_t stream) {
+  if (Cpad % 8 || Cpad < C) return STF_EINVAL;
+  const long units = (long)N * H * W * (Cpad / 8);
+  hipLaunchKernelGGL(pack_input_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream, x, N, C, H,
+                     W, Cpad, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad, void* out,
+                               stf_stream_t stream) {
+  if (mode < 0 || mode > 4 || (mode == 0 && cpad < d1)) return STF_EINVAL;
+  const long total = mode == 0 ? (long)d0 * R * S * cpad : (long)d0 * d1 * R * S;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total, 4096)), dim3(NT), 0, (hipStream_t)stream, w, d0, d1,
+                     R, S, mode, cpad, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_channel_sum(const void* x, int x_cstride, int M, int C, float* partial, float* out,
+                               stf_stream_t stream) {
+  if (C % 8 || NT % (C / 8) || x_cstride % 8) return STF_EINVAL;
+  const long tiles = grid_for((long)M * (C / 8), 1024);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(channel_sum_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)x, x_cstride, (long)M, C,
+                     partial);
+  STF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, (int)tiles, C, out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" const char* stf_error_string(int code) {
+  if (code == STF_EINVAL) return "stfunet: invalid argument (shape/alignment constraint violated)";
+  return hipGetErrorString((hipError_t)code);
+}
+
+extern "C" int stf_abi_version(void) { return 1; }

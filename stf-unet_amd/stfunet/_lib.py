@@ -1,0 +1,102 @@
+"""ctypes binding of the gfx950 C-ABI library (include/stfunet.h).
+
+The library is built in-tree by ``make -C stf-unet_amd/csrc`` (or
+``__graft_entry__.build()``) into ``stfunet/libstfunet_hip.so``.  There is no
+fallback: if the library is missing or fails to load, every op raises.
+``torch`` is imported first so the HIP runtime torch ships (soname
+``libamdhip64.so.7``) is the one our library binds to -- one runtime per process.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstfunet_hip.so")
+
+c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
+                                                ctypes.c_size_t, ctypes.c_int64)
+P = c_void_p
+
+
+class ConvGeom(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("N", "Hs", "Ws", "Cs", "src_cstride", "Hd", "Wd", "R", "S",
+                                     "stride", "pad", "transposed")]
+
+
+class IgemmArgs(ctypes.Structure):
+    _fields_ = [("g", ConvGeom), ("src", P), ("wgt", P), ("Nout", c_int), ("dst", P),
+                ("dst_cstride", c_int), ("bias", P), ("stats", P), ("scatter2x2", c_int)]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [("g", ConvGeom), ("dy", P), ("dy_cstride", c_int), ("Nout", c_int), ("x", P),
+                ("ws", P), ("splits", c_int)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "stf_igemm_mtile": (c_int, [ctypes.POINTER(IgemmArgs)]),
+    "stf_igemm": (c_int, [ctypes.POINTER(IgemmArgs), P]),
+    "stf_wgrad_plan": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_size_t)]),
+    "stf_wgrad": (c_int, [ctypes.POINTER(WgradArgs), P]),
+    "stf_wgrad_reduce": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_channel_sum": (c_int, [P, c_int, c_int, c_int, P, P, P]),
+    "stf_bn_finalize": (c_int, [P, c_int, c_int, c_int, P, P, c_float, c_float, P, P, P, P, P, P, P]),
+    "stf_bn_act": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P, P]),
+    "stf_bn_bwd_tiles": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "stf_bn_bwd_reduce": (c_int, [P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P,
+                                  P, P]),
+    "stf_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P, P, P]),
+    "stf_bn_bwd_apply": (c_int, [P, P, c_int, c_int, c_int, P, P, P, P, P]),
+    "stf_head_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
+    "stf_head_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P, P, P]),
+    "stf_head_tiles": (c_int, [c_int, c_int, c_int, c_int]),
+    "stf_loss_scratch_floats": (c_int, [c_int, c_int]),
+    "stf_loss_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P]),
+    "stf_loss_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P]),
+    "stf_adamw": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_float, c_float, c_float,
+                          P]),
+    "stf_pack_input": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_error_string": (ctypes.c_char_p, [c_int]),
+    "stf_abi_version": (c_int, []),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def load():
+    """Load (once) and return the CDLL; raises RuntimeError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"stfunet HIP library not built ({LIB_PATH}); run `make -C stf-unet_amd/csrc` "
+                           "or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().stf_error_string(rc).decode()
+        raise HipError(f"{what}: {msg} (code {rc})")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def stream():
+    """Raw hipStream_t of torch's current stream on the current device."""
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

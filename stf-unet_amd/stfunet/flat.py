@@ -1,0 +1,82 @@
+"""One flat fp32 buffer for all parameters and one for their gradients.
+
+The modules keep ordinary ``nn.Parameter`` objects (so ``state_dict`` keys and
+``named_parameters`` match the reference), but their storage is re-pointed into
+a single contiguous fp32 buffer.  Backward writes every gradient into the
+matching slice of a flat gradient buffer, so AdamW is one kernel over one
+buffer and the data-parallel all-reduce moves contiguous buckets.
+
+Slices are 16-byte aligned (offsets rounded up to 4 floats) for float4 access;
+the gaps stay zero in both buffers.
+"""
+import torch
+
+
+def _align4(n):
+    return (n + 3) & ~3
+
+
+class FlatParams:
+    def __init__(self, module):
+        self.module = module
+        self.params = [p for p in module.parameters()]
+        self.offsets = []
+        off = 0
+        for p in self.params:
+            self.offsets.append(off)
+            off += _align4(p.numel())
+        self.numel = off
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.data = None
+        self.grad = None
+        self._views = None
+
+    def _aliased(self):
+        if self.data is None:
+            return False
+        base = self.data.data_ptr()
+        for p, off in zip(self.params, self.offsets):
+            if p.device != self.data.device or p.dtype != torch.float32:
+                return False
+            if p.data_ptr() != base + 4 * off or not p.is_contiguous():
+                return False
+        return True
+
+    def ensure(self):
+        """(Re)build the flat buffers if any parameter was re-allocated (``.to()``,
+        ``load_state_dict`` keeps storage, so usually a no-op)."""
+        if self._aliased():
+            return
+        dev = self.params[0].device
+        data = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        for p, off in zip(self.params, self.offsets):
+            n = p.numel()
+            data[off:off + n].copy_(p.detach().reshape(-1).float())
+            p.data = data[off:off + n].view(p.shape)
+        self.data = data
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        self._views = [self.grad[off:off + p.numel()].view(p.shape)
+                       for p, off in zip(self.params, self.offsets)]
+
+    def fresh_grad(self):
+        """Zero the gradient buffer for a new backward.  If a parameter's ``.grad``
+        still aliases it (gradient accumulation without zero_grad), switch to a
+        new buffer so autograd's accumulation adds two distinct tensors."""
+        lo = self.grad.data_ptr()
+        hi = lo + 4 * self.numel
+        if any(p.grad is not None and lo <= p.grad.data_ptr() < hi for p in self.params):
+            self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.grad.device)
+            self._views = [self.grad[off:off + p.numel()].view(p.shape)
+                           for p, off in zip(self.params, self.offsets)]
+        else:
+            self.grad.zero_()
+
+    def grad_view(self, p):
+        return self._views[self.index[id(p)]]
+
+    def grad_views(self):
+        return list(self._views)
+
+    def owns(self, params):
+        """True when ``params`` are exactly this buffer's parameters, in order."""
+        return len(params) == len(self.params) and all(a is b for a, b in zip(params, self.params))

@@ -1,0 +1,220 @@
+"""NHWC bf16 feature maps and thin wrappers over the C-ABI kernels.
+
+A ``Feat`` is a channel slice of an NHWC bf16 buffer: (buffer, N, H, W, C,
+channel stride, channel offset).  Concat buffers are ordinary buffers whose
+slices are written by different producers (virtual concat, no copy).
+
+Every wrapper validates shapes on the host before launching (a kernel that
+walks off a buffer can take the whole GPU down) and launches on torch's
+current stream.  Workspaces come from torch's caching allocator.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import ConvGeom, IgemmArgs, WgradArgs, call, stream
+
+BF16 = torch.bfloat16
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+@dataclass
+class Feat:
+    buf: torch.Tensor      # bf16 storage, >= N*H*W*cs elements
+    N: int
+    H: int
+    W: int
+    C: int
+    cs: int                # channel stride (elements per pixel)
+    off: int = 0           # first channel
+
+    @property
+    def M(self):
+        return self.N * self.H * self.W
+
+    def ptr(self):
+        return ctypes.c_void_p(self.buf.data_ptr() + 2 * self.off)
+
+    def slice(self, c0, c):
+        assert 0 <= c0 and c0 + c <= self.C
+        return Feat(self.buf, self.N, self.H, self.W, c, self.cs, self.off + c0)
+
+    def check(self):
+        assert self.buf.dtype == BF16 and self.buf.is_cuda
+        assert self.buf.numel() >= self.M * self.cs, "feature buffer too small"
+        assert self.off + self.C <= self.cs
+
+    def dense(self):
+        """Debug/test view as a [N, C, H, W] float tensor (copies)."""
+        v = self.buf[: self.M * self.cs].view(self.N, self.H, self.W, self.cs)
+        return v[..., self.off: self.off + self.C].permute(0, 3, 1, 2).float()
+
+
+def new_feat(N, H, W, C, device, cs=None):
+    cs = cs or C
+    return Feat(torch.empty(N * H * W * cs, dtype=BF16, device=device), N, H, W, C, cs, 0)
+
+
+def zeros_feat(N, H, W, C, device, cs=None):
+    cs = cs or C
+    return Feat(torch.zeros(N * H * W * cs, dtype=BF16, device=device), N, H, W, C, cs, 0)
+
+
+# ------------------------------------------------------------------ packs
+def pack_input(x, cpad):
+    """x [N, C, H, W] float -> Feat (NHWC bf16, cpad channels, zero padded)."""
+    x = x.contiguous().float()
+    N, C, H, W = x.shape
+    f = new_feat(N, H, W, cpad, x.device)
+    call("stf_pack_input", _p(x), N, C, H, W, cpad, f.ptr(), stream())
+    return f
+
+
+def pack_weight(w, mode, cpad=0):
+    """fp32 master weight -> bf16 GEMM rows (modes: include/stfunet.h)."""
+    w = w.detach()
+    assert w.dtype == torch.float32 and w.is_contiguous()
+    d0, d1, R, S = w.shape
+    n = d0 * R * S * cpad if mode == 0 else d0 * d1 * R * S
+    out = torch.empty(n, dtype=BF16, device=w.device)
+    call("stf_pack_weight", _p(w), d0, d1, R, S, mode, cpad, _p(out), stream())
+    return out
+
+
+# ------------------------------------------------------------------ implicit GEMM
+def _geom(src: Feat, Hd, Wd, R, S, stride, pad, transposed):
+    return ConvGeom(src.N, src.H, src.W, src.C, src.cs, Hd, Wd, R, S, stride, pad, int(transposed))
+
+
+def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, bias=None,
+          want_stats=False, scatter2x2=False):
+    """Launch stf_igemm; returns the per-tile stats tensor (or None) and tile count."""
+    src.check()
+    dst.check()
+    Hd, Wd = (dst.H // 2, dst.W // 2) if scatter2x2 else (dst.H, dst.W)
+    assert dst.N == src.N
+    assert dst.C == (nout // 4 if scatter2x2 else nout)
+    assert wgt.dtype == BF16 and wgt.numel() == nout * R * S * src.C
+    if transposed:
+        assert stride in (1, 2)
+    else:
+        # every gathered tap must stay inside (or be zero padding of) the source
+        assert (Hd - 1) * stride - pad + R - 1 <= src.H - 1 + pad
+    a = IgemmArgs(_geom(src, Hd, Wd, R, S, stride, pad, transposed), src.ptr(), _p(wgt), nout, dst.ptr(),
+                  dst.cs, _p(bias), None, int(scatter2x2))
+    stats, tiles = None, 0
+    if want_stats:
+        mt = _lib.load().stf_igemm_mtile(ctypes.byref(a))
+        tiles = (src.N * Hd * Wd + mt - 1) // mt
+        stats = torch.empty(tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
+        a.stats = _p(stats)
+    call("stf_igemm", ctypes.byref(a), stream())
+    return stats, tiles
+
+
+def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
+    """Weight gradient into ``out`` (fp32, [dy.C][x.C][R][S] contiguous view)."""
+    dy.check()
+    x.check()
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == dy.C * x.C * R * S
+    g = ConvGeom(x.N, x.H, x.W, x.C, x.cs, dy.H, dy.W, R, S, stride, pad, 0)
+    a = WgradArgs(g, dy.ptr(), dy.cs, dy.C, x.ptr(), None, 0)
+    splits = ctypes.c_int(0)
+    nbytes = ctypes.c_size_t(0)
+    call("stf_wgrad_plan", ctypes.byref(a), ctypes.byref(splits), ctypes.byref(nbytes))
+    ws = torch.empty(nbytes.value // 4, dtype=torch.float32, device=out.device)
+    a.ws = _p(ws)
+    a.splits = splits.value
+    call("stf_wgrad", ctypes.byref(a), stream())
+    call("stf_wgrad_reduce", _p(ws), splits.value, dy.C, R, S, x.C, _p(out), stream())
+
+
+def channel_sum(x: Feat, out):
+    x.check()
+    tiles = min(1024, max(1, (x.M * (x.C // 8) + 255) // 256))
+    part = torch.empty(tiles * x.C, dtype=torch.float32, device=out.device)
+    call("stf_channel_sum", x.ptr(), x.cs, x.M, x.C, _p(part), _p(out), stream())
+
+
+# ------------------------------------------------------------------ BatchNorm
+class BNState:
+    """Per-forward BatchNorm quantities kept for backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "M")
+
+    def __init__(self, C, device, M):
+        t = torch.empty(4 * C, dtype=torch.float32, device=device)
+        self.mean, self.invstd, self.scale, self.shift = t.view(4, C).unbind(0)
+        self.M = M
+
+
+def bn_finalize(stats, tiles, bn, M, training):
+    """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats."""
+    C = bn.num_features
+    st = BNState(C, bn.weight.device, M)
+    mom = 0.1 if bn.momentum is None else bn.momentum
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    call("stf_bn_finalize", _p(stats) if training else None, tiles, C, M, _p(bn.weight.detach()),
+         _p(bn.bias.detach()), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
+         _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
+         stream())
+    if training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    return st
+
+
+def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None):
+    y.check()
+    out.check()
+    assert (y.N, y.H, y.W, y.C) == (out.N, out.H, out.W, out.C)
+    if pooled is not None:
+        pooled.check()
+        assert pooled.cs == pooled.C and pooled.off == 0 and (pooled.H, pooled.W) == (y.H // 2, y.W // 2)
+    call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, _p(st.scale), _p(st.shift), int(relu), out.ptr(),
+         out.cs, pooled.ptr() if pooled is not None else None, stream())
+
+
+def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool: Feat = None, relu=True,
+                dbias=None):
+    """Gradient of relu(BN(y)) [+ maxpool] w.r.t. y; returns dy as a dense Feat.
+
+    ``dz``: grad w.r.t. the BN(+ReLU) output (may be a concat slice);
+    ``dpool``: grad w.r.t. its 2x2 max-pooled output.  dgamma/dbeta/dbias are
+    fp32 views in the flat gradient buffer (dbias: bias of the producing conv).
+    """
+    y.check()
+    C = y.C
+    dev = y.buf.device
+    tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, int(dpool is not None))
+    part = torch.empty(tiles * 2 * C, dtype=torch.float32, device=dev)
+    g = new_feat(y.N, y.H, y.W, C, dev)
+    if dz is not None:
+        dz.check()
+        assert (dz.N, dz.H, dz.W, dz.C) == (y.N, y.H, y.W, C)
+    if dpool is not None:
+        dpool.check()
+        assert dpool.cs == C and dpool.off == 0 and (dpool.H, dpool.W) == (y.H // 2, y.W // 2)
+    call("stf_bn_bwd_reduce", dz.ptr() if dz is not None else None, dz.cs if dz is not None else 0,
+         dpool.ptr() if dpool is not None else None, y.ptr(), y.cs, y.N, y.H, y.W, C, _p(st.scale),
+         _p(st.shift), _p(st.mean), _p(st.invstd), int(relu), g.ptr(), _p(part), stream())
+    return bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias)
+
+
+def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None):
+    C = y.C
+    dev = y.buf.device
+    coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+    call("stf_bn_bwd_finalize", _p(part), tiles, C, y.M, _p(bn.weight.detach()), _p(st.mean),
+         _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
+    bpart = None
+    if dbias is not None:
+        btiles = min(1024, max(1, (y.M * (C // 8) + 255) // 256))
+        bpart = torch.empty(btiles * C, dtype=torch.float32, device=dev)
+    call("stf_bn_bwd_apply", g.ptr(), y.ptr(), y.cs, y.M, C, _p(coef), g.ptr(), _p(bpart), _p(dbias),
+         stream())
+    return g

@@ -1,0 +1,119 @@
+"""AdamW over the flat parameter buffer (one kernel per step).
+
+Drop-in for ``torch.optim.AdamW(params, lr, betas, weight_decay, eps, fused=True)``
+as built at ``train.py:230-237``: a ``torch.optim.Optimizer`` subclass, so
+``LambdaLR`` (``create_lr_scheduler``, train_and_eval.py:414-438), GradScaler and
+``state_dict()`` keep working.  Per-parameter state (``step``, ``exp_avg``,
+``exp_avg_sq``) is exposed as views into two flat buffers.
+
+When the parameters are exactly one model's ``FlatParams`` and their ``.grad``
+tensors are the flat gradient views written by backward, the update is one
+``stf_adamw`` launch over the whole buffer; otherwise gradients are first packed
+into a flat scratch (one copy) and the same kernel runs.
+"""
+import torch
+
+from ._lib import call, stream
+from .nhwc import _p
+
+
+def _align4(n):
+    return (n + 3) & ~3
+
+
+class AdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, fused=None,
+                 **unused):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self._flat = {}
+
+    def _group_buffers(self, gi, group):
+        params = group["params"]
+        key = (gi, tuple(id(p) for p in params))
+        fb = self._flat.get(gi)
+        if fb is not None and fb["key"] == key and fb["pptr"] == [p.data_ptr() for p in params]:
+            return fb
+        offs, off = [], 0
+        for p in params:
+            offs.append(off)
+            off += _align4(p.numel())
+        dev = params[0].device
+        # contiguous parameter storage? (FlatParams lays params out exactly like this)
+        base = params[0].data_ptr()
+        contiguous = all(p.dtype == torch.float32 and p.is_contiguous() and p.device == dev and
+                         p.data_ptr() == base + 4 * o for p, o in zip(params, offs))
+        m = torch.zeros(off, dtype=torch.float32, device=dev)
+        v = torch.zeros(off, dtype=torch.float32, device=dev)
+        for p, o in zip(params, offs):
+            st = self.state[p]
+            n = p.numel()
+            if "exp_avg" in st:                       # resumed / pre-existing state
+                m[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+            st["exp_avg"] = m[o:o + n].view(p.shape)
+            st["exp_avg_sq"] = v[o:o + n].view(p.shape)
+            if "step" not in st:
+                st["step"] = torch.zeros((), dtype=torch.float32)
+        pflat = None
+        if contiguous:
+            pflat = torch.empty(0, dtype=torch.float32, device=dev)
+            pflat.set_(params[0].untyped_storage(), params[0].storage_offset(), (off,))
+        fb = dict(key=key, pptr=[p.data_ptr() for p in params], offs=offs, n=off, m=m, v=v, p=pflat,
+                  gscratch=None)
+        self._flat[gi] = fb
+        return fb
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"]]
+            if not params or all(p.grad is None for p in params):
+                continue
+            if not params[0].is_cuda:
+                raise RuntimeError("stfunet.optim.AdamW runs on the gfx950 kernel only (no CPU fallback)")
+            fb = self._group_buffers(gi, group)
+            b1, b2 = group["betas"]
+            st0 = self.state[params[0]]
+            step = int(st0["step"].item()) + 1
+            for p in params:
+                self.state[p]["step"].fill_(step)
+            bc1 = 1.0 - b1 ** step
+            bc2 = 1.0 - b2 ** step
+            g = self._flat_grad(params, fb)
+            if fb["p"] is not None:
+                call("stf_adamw", _p(fb["p"]), _p(g), _p(fb["m"]), _p(fb["v"]), fb["n"], float(group["lr"]),
+                     float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]), bc1, bc2, stream())
+            else:   # scattered parameters: gather, update, scatter back
+                pf = torch.zeros(fb["n"], dtype=torch.float32, device=params[0].device)
+                for p, o in zip(params, fb["offs"]):
+                    pf[o:o + p.numel()].copy_(p.reshape(-1))
+                call("stf_adamw", _p(pf), _p(g), _p(fb["m"]), _p(fb["v"]), fb["n"], float(group["lr"]),
+                     float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]), bc1, bc2, stream())
+                for p, o in zip(params, fb["offs"]):
+                    p.copy_(pf[o:o + p.numel()].view_as(p))
+        return loss
+
+    def _flat_grad(self, params, fb):
+        g0 = params[0].grad
+        if g0 is not None:
+            base = g0.data_ptr()
+            if all(p.grad is not None and p.grad.is_contiguous() and p.grad.data_ptr() == base + 4 * o
+                   for p, o in zip(params, fb["offs"])):
+                g = torch.empty(0, dtype=torch.float32, device=g0.device)
+                g.set_(g0.untyped_storage(), g0.storage_offset(), (fb["n"],))
+                return g
+        if fb["gscratch"] is None:
+            fb["gscratch"] = torch.zeros(fb["n"], dtype=torch.float32, device=params[0].device)
+        gs = fb["gscratch"]
+        for p, o in zip(params, fb["offs"]):
+            n = p.numel()
+            if p.grad is None:
+                gs[o:o + n].zero_()
+            else:
+                gs[o:o + n].copy_(p.grad.reshape(-1))
+        return gs

@@ -1,0 +1,268 @@
+"""Kernel-level parity of the gfx950 C-ABI against torch fp32 references.
+
+Inputs are rounded to bf16 first, so the reference sees exactly the operands the
+MFMA kernels see; remaining differences are fp32 accumulation order and the
+bf16 rounding of stored outputs (tolerance: relative L2 <= 1e-2 for bf16
+outputs, <= 2e-3 for fp32 outputs/statistics).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def bfr(t):
+    return t.to(torch.bfloat16).float()
+
+
+def feat_from(x, cs=None, off=0):
+    """[N, C, H, W] float -> Feat holding bf16(x) (optionally inside a wider buffer)."""
+    from stfunet.nhwc import Feat
+    N, C, H, W = x.shape
+    cs = cs or C
+    buf = torch.zeros(N, H, W, cs, dtype=torch.bfloat16, device=DEV)
+    buf[..., off:off + C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return Feat(buf.view(-1), N, H, W, C, cs, off)
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("cin,cout,H,stride,R", [(64, 128, 16, 1, 3), (8, 64, 32, 1, 3), (128, 64, 16, 1, 3),
+                                                  (64, 128, 16, 2, 3), (64, 128, 16, 2, 1), (32, 32, 8, 1, 3),
+                                                  (256, 512, 8, 1, 3)])
+def test_conv_forward_stats_and_dgrad(cin, cout, H, stride, R):
+    from stfunet import nhwc
+    pad = R // 2
+    x = bfr(torch.randn(2, cin, H, H + 2, device=DEV))
+    w = bfr(torch.randn(cout, cin, R, R, device=DEV) / (cin * R * R) ** 0.5)
+    b = torch.randn(cout, device=DEV)
+    ref = F.conv2d(x, w, b, stride=stride, padding=pad)
+    src = feat_from(x)
+    Ho, Wo = ref.shape[2:]
+    dst = nhwc.new_feat(2, Ho, Wo, cout, DEV)
+    stats, tiles = nhwc.igemm(src, nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst, R, R, stride, pad,
+                              bias=b, want_stats=True)
+    out = dst.dense()
+    assert rel(out, ref) < 1e-2
+    s = stats.view(tiles, 2, cout).sum(0)
+    assert rel(s[0], out.sum((0, 2, 3))) < 2e-3
+    assert rel(s[1], (out * out).sum((0, 2, 3))) < 2e-3
+    # input gradient through the transposed gather
+    if cin % 8 == 0 and cout % 8 == 0:
+        dy = bfr(torch.randn_like(ref))
+        xr = x.clone().requires_grad_(True)
+        F.conv2d(xr, w, None, stride=stride, padding=pad).backward(dy)
+        dsrc = feat_from(dy)
+        dx = nhwc.new_feat(2, H, H + 2, cin, DEV)
+        nhwc.igemm(dsrc, nhwc.pack_weight(w.contiguous(), 1), cin, dx, R, R, stride, pad, transposed=True)
+        assert rel(dx.dense(), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("cin,cout,H,stride,R,pad", [(64, 128, 16, 1, 3, 1), (8, 64, 32, 1, 3, 1),
+                                                     (64, 128, 16, 2, 3, 1), (64, 64, 16, 2, 1, 0),
+                                                     (256, 256, 8, 1, 3, 1), (8, 64, 16, 2, 7, 3)])
+def test_wgrad(cin, cout, H, stride, R, pad):
+    from stfunet import nhwc
+    x = bfr(torch.randn(2, cin, H, H, device=DEV))
+    w = torch.randn(cout, cin, R, R, device=DEV).requires_grad_(True)
+    y = F.conv2d(x, w, stride=stride, padding=pad)
+    dy = bfr(torch.randn_like(y))
+    y.backward(dy)
+    out = torch.empty(cout * cin * R * R, device=DEV)
+    nhwc.wgrad(feat_from(dy), feat_from(x), R, R, stride, pad, out)
+    assert rel(out.view_as(w), w.grad) < 2e-3
+
+
+def test_conv_into_concat_slice():
+    from stfunet import nhwc
+    x = bfr(torch.randn(2, 64, 8, 8, device=DEV))
+    w = bfr(torch.randn(32, 64, 3, 3, device=DEV) / 24)
+    ref = F.conv2d(x, w, padding=1)
+    cat = nhwc.zeros_feat(2, 8, 8, 96, DEV)
+    nhwc.igemm(feat_from(x, cs=72, off=8), nhwc.pack_weight(w.contiguous(), 0, 64), 32, cat.slice(64, 32),
+               3, 3, 1, 1)
+    full = cat.dense()
+    assert rel(full[:, 64:], ref) < 1e-2
+    assert full[:, :64].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("cin,cout,h", [(128, 64, 8), (1024, 512, 4), (64, 32, 16)])
+def test_convT2x2_fwd_dgrad_wgrad(cin, cout, h):
+    from stfunet import nhwc
+    x = bfr(torch.randn(2, cin, h, h, device=DEV))
+    w = bfr(torch.randn(cin, cout, 2, 2, device=DEV) / cin ** 0.5).requires_grad_(True)
+    b = torch.randn(cout, device=DEV)
+    xr = x.clone().requires_grad_(True)
+    ref = F.conv_transpose2d(xr, w, b, stride=2)
+    dst = nhwc.zeros_feat(2, 2 * h, 2 * h, 2 * cout, DEV)
+    nhwc.igemm(feat_from(x), nhwc.pack_weight(w.detach().contiguous(), 2), 4 * cout, dst.slice(0, cout), 1, 1,
+               1, 0, bias=b, scatter2x2=True)
+    assert rel(dst.dense()[:, :cout], ref) < 1e-2
+    dy = bfr(torch.randn_like(ref))
+    ref.backward(dy)
+    dyf = feat_from(dy)
+    dx = nhwc.new_feat(2, h, h, cin, DEV)
+    nhwc.igemm(dyf, nhwc.pack_weight(w.detach().contiguous(), 3), cin, dx, 2, 2, 2, 0)
+    assert rel(dx.dense(), xr.grad) < 1e-2
+    dw = torch.empty(cin * cout * 4, device=DEV)
+    nhwc.wgrad(feat_from(x), dyf, 2, 2, 2, 0, dw)
+    assert rel(dw.view_as(w), w.grad) < 2e-3
+    db = torch.empty(cout, device=DEV)
+    nhwc.channel_sum(dyf, db)
+    assert rel(db, dy.sum((0, 2, 3))) < 2e-3
+
+
+def test_convT3x3_s2_gather():
+    from stfunet import nhwc
+    x = bfr(torch.randn(2, 64, 8, 8, device=DEV))
+    w = bfr(torch.randn(64, 32, 3, 3, device=DEV) / 24)
+    b = torch.randn(32, device=DEV)
+    ref = F.conv_transpose2d(x, w, b, stride=2, padding=1, output_padding=1)
+    dst = nhwc.new_feat(2, 16, 16, 32, DEV)
+    nhwc.igemm(feat_from(x), nhwc.pack_weight(w.contiguous(), 4), 32, dst, 3, 3, 2, 1, transposed=True, bias=b)
+    assert rel(dst.dense(), ref) < 1e-2
+
+
+class _BN:
+    def __init__(self, C):
+        self.bn = torch.nn.BatchNorm2d(C).to(DEV)
+        with torch.no_grad():
+            self.bn.weight.uniform_(0.5, 1.5)
+            self.bn.bias.uniform_(-0.5, 0.5)
+
+
+@pytest.mark.parametrize("pool", [False, True])
+def test_bn_forward_backward(pool):
+    from stfunet import nhwc
+    C, H = 64, 16
+    y = bfr(torch.randn(2, C, H, H, device=DEV) * 2 + 0.5)
+    m = _BN(C)
+    ref_bn = torch.nn.BatchNorm2d(C).to(DEV)
+    ref_bn.load_state_dict(m.bn.state_dict())
+    yr = y.clone().requires_grad_(True)
+    a_ref = F.relu(ref_bn(yr))
+    yf = feat_from(y)
+    s = y.sum((0, 2, 3))
+    s2 = (y * y).sum((0, 2, 3))
+    stats = torch.stack([s, s2]).contiguous().view(-1)
+    st = nhwc.bn_finalize(stats, 1, m.bn, yf.M, training=True)
+    assert rel(m.bn.running_mean, ref_bn.running_mean) < 1e-5
+    assert rel(m.bn.running_var, ref_bn.running_var) < 1e-5
+    out = nhwc.zeros_feat(2, H, H, 2 * C, DEV)
+    pooled = nhwc.new_feat(2, H // 2, H // 2, C, DEV) if pool else None
+    nhwc.bn_act(yf, st, out.slice(C, C), pooled=pooled)
+    assert rel(out.dense()[:, C:], a_ref) < 1e-2
+    if pool:
+        # pool the bf16-rounded activations (straight-through) so ties break like the kernel
+        a_q = a_ref + (bfr(a_ref) - a_ref).detach()
+        p_ref = F.max_pool2d(a_q, 2)
+        assert rel(pooled.dense(), p_ref) < 1e-2
+        dp = bfr(torch.randn_like(p_ref))
+        dz = bfr(torch.randn_like(a_ref))
+        # route through the kernel's own bf16 activations (tie-breaking matches)
+        (p_ref * dp).sum().add((a_ref * dz).sum()).backward()
+        dzf = nhwc.zeros_feat(2, H, H, 2 * C, DEV).slice(C, C)
+        dzf.buf.view(2, H, H, 2 * C)[..., C:] = dz.permute(0, 2, 3, 1).to(torch.bfloat16)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        dy = nhwc.bn_backward(yf, st, m.bn, dg, db, dz=dzf, dpool=feat_from(dp))
+    else:
+        dz = bfr(torch.randn_like(a_ref))
+        a_ref.backward(dz)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        dy = nhwc.bn_backward(yf, st, m.bn, dg, db, dz=feat_from(dz))
+    assert rel(dg, ref_bn.weight.grad) < 2e-2
+    assert rel(db, ref_bn.bias.grad) < 2e-2
+    assert rel(dy.dense(), yr.grad) < 2e-2
+
+
+def test_head_and_loss():
+    from stfunet import _lib, nhwc
+    from stfunet._lib import call, stream
+    from oracle import loss as o_loss
+    N, C, H, W, K = 2, 64, 16, 16, 2
+    y = bfr(torch.randn(N, C, H, W, device=DEV))
+    m = _BN(C)
+    wt = torch.randn(K, C, device=DEV) / 8
+    bias = torch.randn(K, device=DEV)
+    target = (torch.rand(N, H, W, device=DEV) > 0.7).long()
+    yf = feat_from(y)
+    stats = torch.stack([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3))]).contiguous().view(-1)
+    st = nhwc.bn_finalize(stats, 1, m.bn, yf.M, training=False)
+    logits = torch.empty(N, K, H, W, device=DEV)
+    p = lambda t: nhwc._p(t)  # noqa: E731
+    call("stf_head_fwd", yf.ptr(), N, H, W, C, p(st.scale), p(st.shift), p(wt), p(bias), K, p(logits), stream())
+    yr = y.clone().requires_grad_(True)
+    wr = wt.clone().requires_grad_(True)
+    br = bias.clone().requires_grad_(True)
+    a = F.relu(yr * st.scale.view(1, -1, 1, 1) + st.shift.view(1, -1, 1, 1))
+    ref = F.conv2d(a, wr.view(K, C, 1, 1), br)
+    assert rel(logits, ref) < 1e-4
+    # loss forward / backward vs the oracle criterion
+    lg = logits.clone().requires_grad_(True)
+    ref_loss = o_loss.criterion(lg, target)
+    ref_loss.backward()
+    terms = torch.empty(_lib.load().stf_loss_scratch_floats(N, K), device=DEV)
+    loss = torch.empty(1, device=DEV)
+    call("stf_loss_fwd", p(logits), p(target), N, H, W, K, p(terms), p(loss), stream())
+    assert abs(loss.item() - ref_loss.item()) < 1e-5
+    dl = torch.empty_like(logits)
+    go = torch.ones(1, device=DEV)
+    call("stf_loss_bwd", p(logits), p(target), N, H, W, K, p(terms), p(go), p(dl), stream())
+    assert rel(dl, lg.grad) < 1e-4
+    # head backward
+    z = yr * st.scale.view(1, -1, 1, 1) + st.shift.view(1, -1, 1, 1)
+    gref = torch.autograd.grad(ref, a, dl, retain_graph=True)[0] * (z > 0)
+    ref.backward(dl)
+    tiles = _lib.load().stf_head_tiles(N, H, W, C)
+    g = nhwc.new_feat(N, H, W, C, DEV)
+    bnp = torch.empty(tiles * 2 * C, device=DEV)
+    hp = torch.empty((tiles + 1) * K * (C + 1), device=DEV)
+    dw, dbias = torch.empty(K * C, device=DEV), torch.empty(K, device=DEV)
+    call("stf_head_bwd", p(dl), yf.ptr(), N, H, W, C, p(st.scale), p(st.shift), p(st.mean), p(st.invstd),
+         p(wt), K, g.ptr(), p(bnp), p(hp), p(dw), p(dbias), stream())
+    assert rel(dw.view(K, C), wr.grad) < 1e-4
+    assert rel(dbias, br.grad) < 1e-4
+    assert rel(g.dense(), gref) < 1e-2
+
+
+def test_loss_saturated_empty_set():
+    from stfunet import _lib
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
+    from oracle import loss as o_loss
+    logits = torch.zeros(2, 2, 4, 4, device=DEV)
+    logits[:, 0] = 200.0
+    logits[:, 1] = -200.0
+    target = torch.zeros(2, 4, 4, dtype=torch.long, device=DEV)
+    terms = torch.empty(_lib.load().stf_loss_scratch_floats(2, 2), device=DEV)
+    loss = torch.empty(1, device=DEV)
+    call("stf_loss_fwd", _p(logits), _p(target), 2, 4, 4, 2, _p(terms), _p(loss), stream())
+    ref = o_loss.criterion(logits, target).item()
+    assert abs(loss.item() - ref) < 1e-6
+
+
+def test_adamw_flat_matches_oracle():
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
+    from oracle.optim import adamw_step
+    n = 10007
+    p0 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.randn(n, device=DEV) * 0.1
+    v = torch.rand(n, device=DEV) * 0.1
+    pr, mr, vr = p0.clone(), m.clone(), v.clone()
+    adamw_step([pr], [g], [mr], [vr], 3, lr=1e-3)
+    b1, b2 = 0.9, 0.999
+    call("stf_adamw", _p(p0), _p(g), _p(m), _p(v), n, 1e-3, b1, b2, 1e-8, 1e-4, 1 - b1 ** 3, 1 - b2 ** 3, stream())
+    assert rel(p0, pr) < 1e-6 and rel(m, mr) < 1e-6 and rel(v, vr) < 1e-6

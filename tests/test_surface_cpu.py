@@ -1,0 +1,94 @@
+"""CPU checks of the drop-in surface and the C ABI (no kernel launches)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, REPO
+from oracle import unet as o_unet
+
+
+@pytest.mark.parametrize("base_c,in_ch", [(64, 8), (8, 8), (64, 11)])
+def test_unet_state_dict_matches_reference_keys(base_c, in_ch):
+    from stfunet.unet import UNet
+    m = UNet(in_channels=in_ch, num_classes=2, base_c=base_c)
+    sd = m.state_dict()
+    ref = o_unet.param_shapes(in_ch, 2, base_c)
+    assert list(sd.keys()) == list(ref.keys())
+    for k, shp in ref.items():
+        assert tuple(sd[k].shape) == tuple(shp), k
+    assert len(sd) == 136
+    assert UNet.input_format == "flat_channels"
+    if base_c == 64 and in_ch == 8:
+        # SURVEY.md section 6 quotes 31,042,434, the count for in_channels=1 (enc1.0 has 64*1*9)
+        assert sum(p.numel() for p in m.parameters()) == 31_046_466
+
+
+def test_unet_refuses_cpu_fallback():
+    from stfunet.unet import UNet
+    m = UNet(8, 2, 8)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.zeros(1, 8, 32, 32))
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, "include", "stfunet.h")).read()
+    return sorted(set(re.findall(r"\b(stf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from stfunet import _lib
+    lib = _lib.load()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
+    assert set(syms) == set(_lib.EXPORTED)
+    assert lib.stf_abi_version() == 1
+    assert b"invalid argument" in lib.stf_error_string(100001)
+
+
+def test_library_rejects_bad_shapes_without_launch():
+    from stfunet import _lib
+    lib = _lib.load()
+    g = _lib.ConvGeom(1, 8, 8, 12, 12, 8, 8, 3, 3, 1, 1, 0)      # Cs=12: not a multiple of 8
+    a = _lib.IgemmArgs(g, None, None, 64, None, 64, None, None, 0)
+    assert lib.stf_igemm(ctypes.byref(a), None) == 100001
+    assert lib.stf_bn_act(None, 8, 1, 4, 4, 12, None, None, 1, None, 12, None, None) == 100001
+
+
+def test_preprocess_and_lr_schedule_match_reference():
+    from stfunet import engine
+    from stfunet.unet import UNet
+    x = torch.randn(2, 8, 1, 16, 16)
+    assert engine.preprocess_input(x, UNet(8, 2, 8)).shape == (2, 8, 16, 16)
+    assert engine.preprocess_input(x, object()).shape == x.shape
+    g = np.load(os.path.join(GOLDEN, "lr_table.npz"))
+    f = engine.lr_lambda(10, 3)
+    assert np.allclose([f(i) for i in range(30)], g["lr"], atol=1e-12)
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=1.0)
+    sch = engine.create_lr_scheduler(opt, 10, 3)
+    got = []
+    for _ in range(30):
+        got.append(opt.param_groups[0]["lr"])
+        opt.step()
+        sch.step()
+    assert np.allclose(got, g["lr"], atol=1e-12)
+
+
+def test_engine_metrics_match_reference():
+    from stfunet import engine
+    g = np.load(os.path.join(GOLDEN, "metrics_kat.npz"))
+    logits, target = torch.from_numpy(g["logits"]), torch.from_numpy(g["target"])
+    cm = engine.ConfusionMatrix(2)
+    cm.update(target.flatten(), logits.argmax(1).flatten())
+    assert np.array_equal(cm.mat.numpy(), g["confmat"])
+    dc = engine.DiceCoefficient(2, ignore_index=255)
+    dc.update(logits, target)
+    dc.update(torch.from_numpy(g["logits_absent"]), torch.from_numpy(g["target_absent"]))
+    assert np.allclose(dc.compute().numpy(), g["dice_per_class"], atol=1e-6)
+    assert abs(dc.value.item() - float(g["dice_value"])) < 1e-6
