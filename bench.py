@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark (BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model unet|stf] ...
+
+Default workload = BASELINE.json configs[1]: 2-D UNet(in=8, base_c=64), 256x256
+DCE frames, batch 64 per GPU, bf16 compute (fp32 master weights / statistics),
+one step = forward + CE+Dice criterion + backward (+ RCCL gradient all-reduce
+when N > 1) + AdamW + LambdaLR step, exactly train_one_epoch's step
+(train_utils/train_and_eval.py:384-409).  Inputs are synthetic seeded DCE stacks
+already resident in HBM.  For N > 1 the driver launches one process per GPU via
+torch.distributed.run; every rank keeps its own batch (weak scaling) and the
+timed region is bracketed by barrier + synchronize, max over ranks.
+
+Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant
+kernel family (stf_igemm, timed with HIP events on its launch stream inside the
+timed region) and the CPU baseline (the fp32 oracle restatement timed on this
+host's cores on a bounded sample: the cpu_baseline leg is the only place bench.py
+touches oracle/).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "stf-unet_amd"))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="unet", choices=["unet"])
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--time-steps", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--no-kernel-timer", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """fp32 oracle (plain PyTorch CPU restatement of src/unet.py + criterion +
+    AdamW) on a bounded sample: B=2 at the same 256x256 frames."""
+    from oracle import loss as o_loss, optim as o_optim, unet as o_unet
+    from oracle.init import canonical_state_dict
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    b = 2
+    sd = canonical_state_dict(o_unet.template_state_dict(args.time_steps, 2, 64), seed=0)
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    names = [k for k in p if p[k].requires_grad]
+    m = [torch.zeros_like(p[k]) for k in names]
+    v = [torch.zeros_like(p[k]) for k in names]
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(b, args.time_steps, args.size, args.size, generator=g)
+    t = (torch.rand(b, args.size, args.size, generator=g) > 0.8).long()
+
+    def step(i):
+        for k in names:
+            p[k].grad = None
+        loss = o_loss.criterion(o_unet.forward(p, x, training=True)["out"], t)
+        loss.backward()
+        with torch.no_grad():
+            o_optim.adamw_step([p[k] for k in names], [p[k].grad for k in names], m, v, i, lr=1e-3)
+
+    step(1)
+    t0 = time.perf_counter()
+    for i in range(args.cpu_steps):
+        step(i + 2)
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {"value": round(b / dt, 4), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"oracle fp32 UNet(in={args.time_steps}, base_c=64) train step, batch {b}, "
+                      f"{args.size}x{args.size}, {args.cpu_steps} timed steps after 1 warm-up, "
+                      f"{dt:.3f} s/step"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from stfunet import engine, nhwc
+    from stfunet.ddp import GradAllReduce
+    from stfunet.optim import AdamW
+    from stfunet.synthetic import dce_batch
+    from stfunet.unet import UNet
+
+    torch.manual_seed(1234)
+    model = UNet(in_channels=args.time_steps, num_classes=2, base_c=64).to(dev)
+    model.train()
+    opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
+    steps_total = args.warmup + args.steps
+    sched = engine.create_lr_scheduler(opt, max(steps_total, 1), 10, warmup=True)
+    ddp = GradAllReduce(model) if world > 1 else None
+
+    # synthetic batches resident in HBM before the timed region
+    batches = [dce_batch(args.batch, args.time_steps, args.size, args.size, seed=1000 * rank + i, device=dev)
+               for i in range(2)]
+    batches = [(engine.preprocess_input(x, model), t) for x, t in batches]
+
+    def train_step(i):
+        x, t = batches[i % len(batches)]
+        loss = engine.criterion(model(x), t)
+        opt.zero_grad()
+        loss.backward()
+        if ddp is not None:
+            ddp.finish()
+        opt.step()
+        sched.step()
+        return loss
+
+    for i in range(args.warmup):
+        loss = train_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_kernel_timer:
+        nhwc.TIMER = nhwc.KernelTimer()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = train_step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = nhwc.TIMER.summary() if nhwc.TIMER is not None else {}
+    nhwc.TIMER = None
+    last_loss = float(loss.item())
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    samples = args.batch * world * args.steps
+    value = samples / elapsed
+    if rank == 0:
+        from oracle.unet import train_flops_per_sample
+        train_gflop = train_flops_per_sample(args.time_steps, 64, args.size, args.size) / 1e9
+        roof = None
+        if "igemm" in kt:
+            k = kt["igemm"]
+            per_launch = k["flops"] / k["launches"] / 1e12
+            roof = {"bound": "mfma", "kernel": "stf_igemm (conv fwd + dgrad + convT, all launches)",
+                    "achieved": round(k["tflops"], 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
+                    "avg_algorithmic_tflop_per_launch": round(per_launch, 6)}
+        res = {
+            "metric": "training samples/sec (256x256 DCE-MRI frames)",
+            "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
+            "config": {"workload": f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step",
+                       "model": "UNet", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "seq_len": args.time_steps, "image": [args.size, args.size],
+                       "parallelism": f"dp{world}"},
+            "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
+            "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
+            "roofline": roof,
+            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in d.items()}
+                        for k, d in kt.items()},
+            "last_loss": round(last_loss, 5),
+        }
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

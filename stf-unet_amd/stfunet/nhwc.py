@@ -23,6 +23,37 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+class KernelTimer:
+    """Brackets kernel launches with HIP events on the launching stream and
+    accumulates algorithmic FLOPs per kernel family (bench.py's roofline)."""
+
+    def __init__(self):
+        self.rec = {}
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        return ev
+
+    def end(self, ev0, family, flops):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record(torch.cuda.current_stream())
+        self.rec.setdefault(family, []).append((ev0, ev1, flops))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for fam, items in self.rec.items():
+            ms = sum(a.elapsed_time(b) for a, b, _ in items)
+            fl = sum(f for _, _, f in items)
+            out[fam] = dict(launches=len(items), ms=ms, flops=fl,
+                            avg_us=1e3 * ms / len(items), tflops=fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0)
+        return out
+
+
+TIMER = None   # set to a KernelTimer to instrument igemm / wgrad launches
+
+
 @dataclass
 class Feat:
     buf: torch.Tensor      # bf16 storage, >= N*H*W*cs elements
@@ -113,7 +144,12 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         tiles = (src.N * Hd * Wd + mt - 1) // mt
         stats = torch.empty(tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
         a.stats = _p(stats)
+    t = TIMER
+    ev = t.begin() if t is not None else None
     call("stf_igemm", ctypes.byref(a), stream())
+    if t is not None:
+        macs = src.N * Hd * Wd * nout * R * S * src.C
+        t.end(ev, "igemm", 2.0 * macs / (stride * stride if transposed else 1))
     return stats, tiles
 
 
@@ -130,7 +166,11 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
     ws = torch.empty(nbytes.value // 4, dtype=torch.float32, device=out.device)
     a.ws = _p(ws)
     a.splits = splits.value
+    t = TIMER
+    ev = t.begin() if t is not None else None
     call("stf_wgrad", ctypes.byref(a), stream())
+    if t is not None:
+        t.end(ev, "wgrad", 2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad_reduce", _p(ws), splits.value, dy.C, R, S, x.C, _p(out), stream())
 
 

@@ -1,0 +1,42 @@
+"""Seeded synthetic DCE-MRI stacks (BreaDM is not available here).
+
+Shape contract of ``DriveDataset`` + ``collate_fn`` (my_dataset.py:15-244):
+image [B, T, 1, H, W] fp32 normalised like train.py:147-148 (mean 0.709, std
+0.127), mask [B, H, W] int64 in {0, 1}.  Each sample: background N(0.5, 0.3^2)
+plus 1-3 discs (radius 6-40 px at 256^2, scaled with H) whose intensity rises by
+0.25 per unit of normalised time (wash-in).  ``pk_channels`` appends smooth
+random fields in [0, 1] on the T axis (the PK-map layout of
+src/stf_lstm_unet.py:146-156).  ``mask_hw`` nearest-downsamples the mask (the
+STF model predicts at H/2 x W/2).
+"""
+import torch
+
+
+def dce_batch(batch, time_steps, height, width, seed=0, device="cuda", pk_channels=0, mask_hw=None):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    img = 0.5 + 0.3 * torch.randn(batch, time_steps, 1, height, width, generator=g, device=device)
+    yy = torch.arange(height, device=device).view(1, height, 1).float()
+    xx = torch.arange(width, device=device).view(1, 1, width).float()
+    mask = torch.zeros(batch, height, width, dtype=torch.bool, device=device)
+    scale = height / 256.0
+    for _ in range(3):
+        cy = torch.rand(batch, 1, 1, generator=g, device=device) * height
+        cx = torch.rand(batch, 1, 1, generator=g, device=device) * width
+        r = (6 + 34 * torch.rand(batch, 1, 1, generator=g, device=device)) * scale
+        on = torch.rand(batch, 1, 1, generator=g, device=device) < 0.75
+        disc = ((yy - cy) ** 2 + (xx - cx) ** 2 <= r * r) & on
+        mask |= disc
+    ramp = 0.25 * (torch.arange(1, time_steps + 1, device=device).float() / time_steps)
+    img = img + mask.view(batch, 1, 1, height, width).float() * ramp.view(1, -1, 1, 1, 1)
+    img = (img - 0.709) / 0.127
+    if pk_channels:
+        low = torch.rand(batch, pk_channels, 1, max(height // 32, 2), max(width // 32, 2), generator=g,
+                         device=device)
+        pk = torch.nn.functional.interpolate(low.flatten(1, 2), size=(height, width), mode="bilinear",
+                                             align_corners=True).view(batch, pk_channels, 1, height, width)
+        img = torch.cat([img, pk], dim=1)
+    target = mask.long()
+    if mask_hw is not None:
+        target = target[:, :: height // mask_hw[0], :: width // mask_hw[1]].contiguous()
+    return img.contiguous(), target

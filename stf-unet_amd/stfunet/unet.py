@@ -108,7 +108,15 @@ class UNetProgram:
         self.ups = [model.up4, model.up3, model.up2, model.up1]
         self.decs = [DoubleConvProgram(b) for b in (model.dec4, model.dec3, model.dec2, model.dec1)]
         self.flat = FlatParams(model)
-        self.grad_ready_hook = None       # called with (flat_offset_begin, flat_offset_end) as grads land
+        # grad_ready_hook(begin): flat-gradient elements [begin, numel) are final.  Backward
+        # finishes blocks in exactly the reverse of registration (= flat) order, so the
+        # finished gradients always form a suffix of the flat buffer (DDP buckets).
+        self.grad_ready_hook = None
+
+    def _done(self, module):
+        if self.grad_ready_hook is not None:
+            first = next(module.parameters())
+            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
@@ -181,6 +189,7 @@ class UNetProgram:
         dy2 = nhwc.bn_backward_from_partial(g, s.y2, s.bn2, dec1.blk[4], bnp, tiles, gv(dec1.blk[4].weight),
                                             gv(dec1.blk[4].bias), gv(dec1.blk[3].bias))
         dcat = dec1.backward(s, self.flat, True, dy2=dy2)
+        self._done(dec1.blk)
         dcats = [None] * 4
         dcats[0] = dcat
         # decoder levels 2..4 and the up-convs, deepest last
@@ -194,17 +203,21 @@ class UNetProgram:
             nhwc.channel_sum(dup, gv(up.bias))
             dsrc = new_feat(src.N, src.H, src.W, src.C, dev)
             nhwc.igemm(dup, nhwc.pack_weight(up.weight, 3), src.C, dsrc, 2, 2, 2, 0)
+            self._done(up)
             if i > 0:
                 dcats[4 - i] = self.decs[i - 1].backward(S.dec[i - 1], self.flat, True, dz=dsrc)
+                self._done(self.decs[i - 1].blk)
             else:
                 d_b = dsrc
         dpool = self.bott.backward(S.bott, self.flat, True, dz=d_b)
+        self._done(self.bott.blk)
         for j in (3, 2, 1, 0):
             lvl = self.levels[j]
             C = lvl.cout
             dskip = dcats[j].slice(C, C)
             dpool = lvl.backward(S.enc[j], self.flat, j > 0, dz=dskip, dpool=dpool)
             dcats[j] = None
+            self._done(lvl.blk)
 
 
 class _UNetFunction(torch.autograd.Function):
@@ -223,7 +236,7 @@ class _UNetFunction(torch.autograd.Function):
         prog.backward(ctx.saved, dlogits)
         ctx.saved = None
         if prog.grad_ready_hook is not None:
-            prog.grad_ready_hook(0, prog.flat.numel)
+            prog.grad_ready_hook(0)
         return (None, None, *prog.flat.grad_views())
 
 
