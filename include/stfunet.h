@@ -90,8 +90,10 @@ int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_bytes);
  *   replaces the weight gradient of every Conv2d/ConvTranspose2d above. */
 int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream);
 /* Sum `splits` slabs into out[Nout][Cs][R][S] (PyTorch Conv2d weight layout;
- * for ConvTranspose2d pass Nout=Cin, Cs=Cout and get [Cin][Cout][R][S]). */
-int stf_wgrad_reduce(const float* ws, int splits, int Nout, int R, int S, int Cs,
+ * for ConvTranspose2d pass Nout=Cin, Cs=Cout and get [Cin][Cout][R][S]).
+ * Partial-slab arguments of this and the *_finalize / channel-sum functions are
+ * scratch: they are reduced in place (fixed order) and left clobbered. */
+int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs,
                      float* out, stf_stream_t stream);
 
 /* Per-channel column sums of a bf16 NHWC tensor (bias gradients of ConvT /
@@ -104,7 +106,7 @@ int stf_channel_sum(const void* x, int x_cstride, int M, int C, float* partial,
  * ResNet bn1/bn2/downsample.1): batch mean, biased variance for normalisation,
  * unbiased variance into running_var, momentum 0.1, eps 1e-5 (torch defaults).
  * stats == NULL selects eval mode (normalise with running_mean/var, no update). */
-int stf_bn_finalize(const float* stats, int tiles, int C, int M, const float* gamma,
+int stf_bn_finalize(float* stats, int tiles, int C, int M, const float* gamma,
                     const float* beta, float momentum, float eps, float* running_mean,
                     float* running_var, float* mean, float* invstd, float* scale,
                     float* shift, stf_stream_t stream);
@@ -123,7 +125,7 @@ int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const v
                       const float* shift, const float* mean, const float* invstd,
                       int relu, void* g_out, float* partial, stf_stream_t stream);
 /* dgamma, dbeta and the per-channel coefficients of dy = A*g + B*y + C. */
-int stf_bn_bwd_finalize(const float* partial, int tiles, int C, int M, const float* gamma,
+int stf_bn_bwd_finalize(float* partial, int tiles, int C, int M, const float* gamma,
                         const float* mean, const float* invstd, float* dgamma, float* dbeta,
                         float* coef, stf_stream_t stream);
 /* dy = A*g + B*y + C (bf16 [M][C]); optional per-tile column sums of dy for
@@ -181,7 +183,9 @@ int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* o
  *          the transposed gather indexes taps directly)
  *  mode 2: ConvT  w[Ci][Co][R][S]       -> [(r*S+s)*Co+co][Ci] (scatter2x2 fwd)
  *  mode 3: ConvT  w[Ci][Co][R][S]       -> [Ci][R][S][Co]      (ConvT dgrad)
- *  mode 4: ConvT  w[Ci][Co][R][S]       -> [Co][R][S][Ci]      (ConvT fwd gather) */
+ *  mode 4: ConvT  w[Ci][Co][R][S]       -> [Co][R][S][Ci]      (ConvT fwd gather)
+ *  mode 5: Conv2d w[Co][Ci][R][S]       -> [Ci][R-1-r][S-1-s][Co] (stride-1 dgrad as a
+ *          forward gather with pad' = R-1-pad) */
 int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad,
                     void* out, stf_stream_t stream);
 

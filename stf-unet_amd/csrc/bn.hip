@@ -15,6 +15,7 @@
 // and the two sums; stf_bn_bwd_apply evaluates the affine form in place.
 #include "common.h"
 #include "../../include/stfunet.h"
+#include "reduce.h"
 
 namespace {
 
@@ -283,9 +284,10 @@ __global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles
 
 static bool cg_ok(int C) { return C % 8 == 0 && NT % (C / 8) == 0; }
 
-extern "C" int stf_bn_finalize(const float* stats, int tiles, int C, int M, const float* gamma, const float* beta,
+extern "C" int stf_bn_finalize(float* stats, int tiles, int C, int M, const float* gamma, const float* beta,
                                float momentum, float eps, float* running_mean, float* running_var, float* mean,
                                float* invstd, float* scale, float* shift, stf_stream_t stream) {
+  if (stats) tiles = stf::colsum_stage1(stats, tiles, 2L * C, (hipStream_t)stream);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, stats, tiles,
                      C, M, gamma, beta, momentum, eps, running_mean, running_var, mean, invstd, scale, shift);
   STF_CHECK_LAUNCH();
@@ -337,9 +339,10 @@ extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpo
   return 0;
 }
 
-extern "C" int stf_bn_bwd_finalize(const float* partial, int tiles, int C, int M, const float* gamma,
+extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int C, int M, const float* gamma,
                                    const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
                                    stf_stream_t stream) {
+  tiles = stf::colsum_stage1(partial, tiles, 2L * C, (hipStream_t)stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, partial,
                      tiles, C, M, gamma, mean, invstd, dgamma, dbeta, coef);
   STF_CHECK_LAUNCH();
@@ -355,7 +358,8 @@ extern "C" int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int
                      y_cstride, (long)M, C, coef, (uint16_t*)dy, bias_partial);
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
-    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias_partial, tiles, C, dbias);
+    const int S = stf::colsum_stage1(bias_partial, tiles, C, s);
+    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
   return 0;

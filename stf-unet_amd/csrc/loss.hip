@@ -11,6 +11,7 @@
 //   G_k = -(1/(K*B)) dD/dp = -(1/(K*B)) (2 t/(S+eps) - (2I+eps)/(S+eps)^2).
 #include "common.h"
 #include "../../include/stfunet.h"
+#include "reduce.h"
 
 namespace {
 
@@ -325,7 +326,8 @@ extern "C" int stf_head_bwd(const float* dlogits, const void* y, int N, int H, i
   STF_CHECK_LAUNCH();
   const int HC = classes * (C + 1);
   // reduce [tiles][K*(C+1)] into row `tiles` of the slab, then split into dw[K*C], db[K]
-  hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, tiles, HC,
+  const int S = stf::colsum_stage1(head_partial, tiles, HC, s);
+  hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, S, HC,
                      head_partial + (size_t)tiles * HC);
   STF_CHECK_LAUNCH();
   hipError_t e = hipMemcpyAsync(dw, head_partial + (size_t)tiles * HC, sizeof(float) * classes * C,

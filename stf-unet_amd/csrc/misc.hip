@@ -2,6 +2,7 @@
 // GEMM rows), per-channel column sums, and the error-string helper.
 #include "common.h"
 #include "../../include/stfunet.h"
+#include "reduce.h"
 
 __global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out);
 
@@ -90,6 +91,12 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int d0, int d1, 
       const long t = o / d1;
       const int tap = (int)(t % RS), ci = (int)(t / RS);
       v = w[((long)ci * d1 + co) * RS + tap];
+    } else if (mode == 5) {     // Conv2d -> [Ci][R-1-r][S-1-s][Co] (stride-1 dgrad as a forward gather)
+      const int co = (int)(o % d0);
+      const long t = o / d0;
+      const int tap = (int)(t % RS), ci = (int)(t / RS);
+      const int r = tap / S, s_ = tap - r * S;
+      v = w[((long)co * d1 + ci) * RS + (R - 1 - r) * S + (S - 1 - s_)];
     } else {                    // mode 4: ConvT -> [Co][R][S][Ci]
       const int ci = (int)(o % d0);
       const long t = o / d0;
@@ -153,7 +160,7 @@ extern "C" int stf_pack_input(const float* x, int N, int C, int H, int W, int Cp
 
 extern "C" int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad, void* out,
                                stf_stream_t stream) {
-  if (mode < 0 || mode > 4 || (mode == 0 && cpad < d1)) return STF_EINVAL;
+  if (mode < 0 || mode > 5 || (mode == 0 && cpad < d1)) return STF_EINVAL;
   const long total = mode == 0 ? (long)d0 * R * S * cpad : (long)d0 * d1 * R * S;
   hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total, 4096)), dim3(NT), 0, (hipStream_t)stream, w, d0, d1,
                      R, S, mode, cpad, (uint16_t*)out);
@@ -169,7 +176,8 @@ extern "C" int stf_channel_sum(const void* x, int x_cstride, int M, int C, float
   hipLaunchKernelGGL(channel_sum_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)x, x_cstride, (long)M, C,
                      partial);
   STF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, (int)tiles, C, out);
+  const int S = stf::colsum_stage1(partial, tiles, C, s);
+  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, S, C, out);
   STF_CHECK_LAUNCH();
   return 0;
 }

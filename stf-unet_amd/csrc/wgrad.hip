@@ -12,6 +12,7 @@
 // slab; stf_wgrad_reduce sums the slabs in a fixed order (deterministic).
 #include "common.h"
 #include "../../include/stfunet.h"
+#include "reduce.h"
 
 namespace {
 
@@ -224,11 +225,12 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   return 0;
 }
 
-extern "C" int stf_wgrad_reduce(const float* ws, int splits, int Nout, int R, int S, int Cs, float* out,
+extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs, float* out,
                                 stf_stream_t stream) {
   const size_t total = (size_t)Nout * R * S * Cs;
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, splits, Nout,
+  const int rows = stf::colsum_stage1(ws, splits, (long)total, (hipStream_t)stream);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, rows, Nout,
                      R, S, Cs, out);
   STF_CHECK_LAUNCH();
   return 0;

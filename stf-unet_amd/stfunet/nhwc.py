@@ -153,6 +153,15 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     return stats, tiles
 
 
+def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad):
+    """Conv2d input gradient: stride 1 runs as a forward gather over flipped taps
+    (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather."""
+    if stride == 1 and 2 * pad == R - 1 and R == S:
+        igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad)
+    else:
+        igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True)
+
+
 def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
     """Weight gradient into ``out`` (fp32, [dy.C][x.C][R][S] contiguous view)."""
     dy.check()

@@ -80,14 +80,14 @@ class DoubleConvProgram:
                                    dbias=gv(conv2.bias))
         nhwc.wgrad(dy2, s.a1, 3, 3, 1, 1, gv(conv2.weight))
         da1 = new_feat(s.a1.N, s.a1.H, s.a1.W, self.cout, s.a1.buf.device)
-        nhwc.igemm(dy2, nhwc.pack_weight(conv2.weight, 1), self.cout, da1, 3, 3, 1, 1, transposed=True)
+        nhwc.conv_dgrad(dy2, conv2.weight, da1, 3, 3, 1, 1)
         dy1 = nhwc.bn_backward(s.y1, s.bn1, bn1, gv(bn1.weight), gv(bn1.bias), dz=da1, dbias=gv(conv1.bias))
         del da1
         self._wgrad_conv1(dy1, s.src, gv(conv1.weight))
         if not need_dsrc:
             return None
         dsrc = new_feat(s.src.N, s.src.H, s.src.W, s.src.C, s.src.buf.device)
-        nhwc.igemm(dy1, nhwc.pack_weight(conv1.weight, 1), s.src.C, dsrc, 3, 3, 1, 1, transposed=True)
+        nhwc.conv_dgrad(dy1, conv1.weight, dsrc, 3, 3, 1, 1)
         return dsrc
 
     def _wgrad_conv1(self, dy1, src, out):
