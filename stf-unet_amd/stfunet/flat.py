@@ -75,7 +75,9 @@ class FlatParams:
         return self._views[self.index[id(p)]]
 
     def grad_views(self):
-        return list(self._views)
+        """Fresh view objects (nothing else references them), so autograd's
+        AccumulateGrad can adopt them as ``p.grad`` without a copy."""
+        return [self.grad[off:off + p.numel()].view(p.shape) for p, off in zip(self.params, self.offsets)]
 
     def owns(self, params):
         """True when ``params`` are exactly this buffer's parameters, in order."""
