@@ -47,6 +47,19 @@ typedef struct stf_conv_geom {
   int transposed;
 } stf_conv_geom;
 
+/* LSTM cell fused into the GEMM epilogue: the GEMM computes the gate
+ * pre-activations [x_t | h_{t-1}] . [W_ih | W_hh]^T with gate-interleaved
+ * columns (column 4c+q = gate q in torch order i, f, g, o, of hidden channel c),
+ * the epilogue adds the bias and applies c_t = f*c_{t-1} + i*g, h_t = o*tanh(c_t)
+ * (nn.LSTM, src/stf_lstm_unet.py:124-127,219-235). */
+typedef struct stf_lstm_epi {
+  const float* c_prev; /* [M][Ch] or NULL (zero initial state)                    */
+  float* c_out;        /* [M][Ch]                                                 */
+  void* h_out;         /* bf16, h_t written with stride h_cstride (may be the next */
+  int h_cstride;       /* step's [x | h] buffer or the decoder's concat slice)     */
+  float* gates;        /* [M][4Ch] activated gates (i, f, g, o), for backward     */
+} stf_lstm_epi;
+
 typedef struct stf_igemm_args {
   stf_conv_geom g;
   const void* src;     /* bf16, first used channel                              */
@@ -60,9 +73,14 @@ typedef struct stf_igemm_args {
   int scatter2x2;      /* 1: ConvTranspose2d(k=2,s=2) epilogue: column          */
                        /* n = (dy*2+dx)*Cout + co lands on pixel (2yd+dy,2xd+dx)*/
                        /* of a [N][2Hd][2Wd] destination                        */
+  int group_rows;      /* >0: M tiles aligned to groups of this many rows and   */
+                       /* stats laid out [M/group_rows][mtiles/group][2][Nout]  */
+                       /* (per-time-step BatchNorm of the batched STF encoder)  */
+  int accumulate;      /* 1: dst += result (bf16 read-modify-write)             */
+  const stf_lstm_epi* lstm; /* non-NULL: LSTM cell epilogue, dst unused          */
 } stf_igemm_args;
 
-/* Rows per M tile chosen for these args (size `stats` as ceil(M/rows)). */
+/* Rows per M tile chosen for these args (size `stats` as groups*ceil(rows_per_group/mtile)). */
 int stf_igemm_mtile(const stf_igemm_args* a);
 /* Conv2d 3x3/1x1/strided forward with fused bias + BatchNorm partial statistics
  *   replaces nn.Conv2d in conv_block  (src/unet.py:12,15), ResidualConvBlock
@@ -102,38 +120,50 @@ int stf_channel_sum(const void* x, int x_cstride, int M, int C, float* partial,
                     float* out, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- BatchNorm2d
- * Training-mode BatchNorm2d + ReLU (src/unet.py:13-17; src/stf_lstm_unet.py:14-17,
+ * Training-mode BatchNorm2d (+ReLU) (src/unet.py:13-17; src/stf_lstm_unet.py:14-17,
  * ResNet bn1/bn2/downsample.1): batch mean, biased variance for normalisation,
  * unbiased variance into running_var, momentum 0.1, eps 1e-5 (torch defaults).
- * stats == NULL selects eval mode (normalise with running_mean/var, no update). */
-int stf_bn_finalize(float* stats, int tiles, int C, int M, const float* gamma,
-                    const float* beta, float momentum, float eps, float* running_mean,
-                    float* running_var, float* mean, float* invstd, float* scale,
-                    float* shift, stf_stream_t stream);
-/* out = relu?(y*scale + shift) into a channel slice; optional fused 2x2 max
- * pool (MaxPool2d(2), src/unet.py:25,41-45) into `pooled` [N][H/2][W/2][C]. */
-int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int C,
-               const float* scale, const float* shift, int relu, void* out,
+ * `groups` splits the N images into equal statistic groups (per-time-step BN of
+ * the batched STF encoder, src/stf_lstm_unet.py:168-186): every group gets its
+ * own mean/invstd/scale/shift ([groups][C]) and running stats advance once per
+ * group, in order.  UNet passes groups = 1.  Partial-slab inputs are consumed. */
+/* stats: [groups][tiles][2][C] from stf_igemm (tiles = per group), or NULL for
+ * eval mode (normalise with running_mean/var, no update). */
+int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64_t M,
+                    const float* gamma, const float* beta, float momentum, float eps,
+                    float* running_mean, float* running_var, float* mean, float* invstd,
+                    float* scale, float* shift, stf_stream_t stream);
+/* out = act(y*scale + shift [+ res | + res*res_scale + res_shift]) into a
+ * channel slice.  Residual: identity shortcut (res_scale NULL) or a BN'd
+ * downsample branch (ResNet BasicBlock src/stf_lstm_unet.py:108-114,
+ * ResidualConvBlock :29-35).  Optional fused 2x2 max pool (MaxPool2d(2),
+ * src/unet.py:25,41-45) into `pooled` [N][H/2][W/2][C] (no residual). */
+int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int C, int groups,
+               const float* scale, const float* shift, int relu, const void* res,
+               int res_cstride, const float* res_scale, const float* res_shift, void* out,
                int out_cstride, void* pooled, stf_stream_t stream);
-/* Backward of BN(+ReLU)(+2x2 max pool):  da = dz + maxpool_bwd(dpool)
- * (either may be NULL), g = relu ? da * (y*scale+shift > 0) : da, written to
- * g_out [M][C]; partial[tile][2][C] = (sum g, sum g*xhat).  Returns tiles via
+/* Backward of BN(+ReLU)(+2x2 max pool):  da = dz + maxpool_bwd(dpool) (either
+ * may be NULL), g = da masked by mask_mode (0 none, 1 ReLU recomputed from
+ * y*scale+shift, 2 mask_src > 0: ReLU after a residual add), written to g_out
+ * [M][C]; partial [groups][tiles][2][C] = (sum g, sum g*xhat), tiles from
  * stf_bn_bwd_tiles. */
-int stf_bn_bwd_tiles(int N, int H, int W, int C, int pooled);
+int stf_bn_bwd_tiles(int N, int H, int W, int C, int groups, int pooled);
 int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const void* y,
-                      int y_cstride, int N, int H, int W, int C, const float* scale,
-                      const float* shift, const float* mean, const float* invstd,
-                      int relu, void* g_out, float* partial, stf_stream_t stream);
-/* dgamma, dbeta and the per-channel coefficients of dy = A*g + B*y + C. */
-int stf_bn_bwd_finalize(float* partial, int tiles, int C, int M, const float* gamma,
-                        const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                        float* coef, stf_stream_t stream);
-/* dy = A*g + B*y + C (bf16 [M][C]); optional per-tile column sums of dy for
- * the bias of the preceding conv (bias_partial [ceil(M/256)][C]) reduced to
- * dbias. */
-int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int M, int C,
-                     const float* coef, void* dy, float* bias_partial, float* dbias,
-                     stf_stream_t stream);
+                      int y_cstride, int N, int H, int W, int C, int groups,
+                      const float* scale, const float* shift, const float* mean,
+                      const float* invstd, int mask_mode, const void* mask_src,
+                      int mask_cstride, void* g_out, float* partial, stf_stream_t stream);
+/* dgamma, dbeta (summed over groups) and coef [groups][3][C] of dy = A*g + B*y + C. */
+int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C, int64_t M,
+                        const float* gamma, const float* mean, const float* invstd,
+                        float* dgamma, float* dbeta, float* coef, stf_stream_t stream);
+/* dy = A*g + B*y + C (bf16, dy_cstride; may alias g when dense); optional
+ * per-tile column sums of dy for the bias of the producing conv
+ * (bias_partial [stf_bn_bwd_apply_tiles][C]) reduced into dbias. */
+int stf_bn_bwd_apply_tiles(int64_t M, int C);
+int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int64_t M, int C,
+                     int groups, const float* coef, void* dy, int dy_cstride,
+                     float* bias_partial, float* dbias, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- head + loss
  * UNet OutConv fused with the last BN+ReLU (src/unet.py:16-17,37,56):
@@ -188,6 +218,37 @@ int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* o
  *          forward gather with pad' = R-1-pad) */
 int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad,
                     void* out, stf_stream_t stream);
+
+/* ---------------------------------------------------------------- STF-LSTM-UNet
+ * x [B][Ttot][C][H][W] fp32 -> t-major NHWC bf16 [T*B][H][W][Cpad]: frame t of
+ * sample b is image t*B+b; channels [0,C) the frame, [C,C+P) the P PK maps
+ * x[b][T+p][0] (src/stf_lstm_unet.py:146-156,172-174), rest zero. */
+int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int T, int P,
+                      int Cpad, void* out, stf_stream_t stream);
+/* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16;
+ * backward gathers dout over the windows whose first maximum is the pixel. */
+int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, stf_stream_t stream);
+int stf_maxpool3s2_bwd(const void* x, const void* dout, int N, int H, int W, int C, void* dx,
+                       stf_stream_t stream);
+/* nn.LSTM(C, C) weights -> gate-interleaved GEMM operands: wcat [4C][2C] (row
+ * 4c+q = torch row q*C+c of [W_ih | W_hh]), wcat_t [2C][4C], bias = b_ih + b_hh
+ * interleaved (src/stf_lstm_unet.py:124-127). */
+int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
+                  int C, void* wcat, void* wcat_t, float* bias, stf_stream_t stream);
+/* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
+int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,
+                         float* dw_hh, float* db_ih, float* db_hh, stf_stream_t stream);
+/* One BPTT step of the LSTM cell: from activated gates [M][4C], c_t, c_{t-1}
+ * (NULL = 0), dh_t (bf16, stride) and dc from step t+1 (NULL = 0) -> dgates
+ * (pre-activation, bf16 [M][4C] interleaved) and dc for step t-1 (may alias dc_in). */
+int stf_lstm_cell_bwd(const float* gates, const float* c_t, const float* c_prev, const void* dh,
+                      int dh_cstride, const float* dc_in, float* dc_out, void* dgates, int64_t M,
+                      int C, stf_stream_t stream);
+/* F.interpolate(pk, (h, w), bilinear, align_corners=True) of the PK maps of x,
+ * written for every time step into channels [coff, coff+P) of dst
+ * [T*B][h][w][dst_cstride] (PK fusion concat, src/stf_lstm_unet.py:189-200). */
+int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int H, int W, int h, int w,
+                  void* dst, int dst_cstride, int coff, stf_stream_t stream);
 
 const char* stf_error_string(int code);
 int stf_abi_version(void);

@@ -1,18 +1,24 @@
-// Training-mode BatchNorm2d (+ReLU, +2x2 max pool) for NHWC bf16 activations.
+// Training-mode BatchNorm2d (+ReLU, +residual add, +2x2 max pool) for NHWC bf16
+// activations, with optional statistic *groups* along the image axis.
 //
-// Forward: the producing conv's epilogue already wrote per-tile (sum, sum^2);
-// stf_bn_finalize folds them (fp64) into mean/invstd, the affine (scale, shift)
-// and the running-stat update; stf_bn_act applies y*scale+shift (+ReLU) while
-// writing into a channel slice of the concat buffer and, optionally, the 2x2
-// max-pooled tensor for the next encoder level -- one read of y, no separate
-// pool or cat pass.
+// Groups: the STF encoder runs all T time steps as one batch of T*B images
+// (t-major), but the reference normalises every time step with its own batch
+// statistics and advances the running statistics once per step
+// (src/stf_lstm_unet.py:168-186).  Group g = images [g*N/G, (g+1)*N/G) keeps its
+// own mean/invstd/scale/shift; running stats are updated group by group in t
+// order, exactly like T sequential BatchNorm calls.  UNet uses G = 1.
 //
-// Backward (per channel, M = N*H*W, xhat = (y-mean)*invstd, g = dL/d(BN out)):
-//   dgamma = sum g*xhat, dbeta = sum g,
-//   dy = gamma*invstd*(g - dbeta/M - xhat*dgamma/M) = A*g + B*y + C.
-// stf_bn_bwd_reduce forms g (ReLU mask and max-pool routing recomputed from y,
-// first maximum of each window in row-major order like torch's CPU kernel)
-// and the two sums; stf_bn_bwd_apply evaluates the affine form in place.
+// Forward: the producing conv's epilogue wrote per-tile (sum, sum^2) for tiles
+// aligned to groups ([G][tpg][2][C]); stf_bn_finalize folds them (fp64) and
+// stf_bn_act applies  out = act(y*scale+shift [+ residual])  where the residual
+// is another bf16 tensor (identity shortcut) or a second BN of a raw conv output
+// (downsample shortcut: ResNet BasicBlock, ResidualConvBlock), optionally also
+// writing the 2x2 max-pooled tensor (UNet Down, src/unet.py:25).
+//
+// Backward (per group and channel, xhat = (y-mean)*invstd):
+//   g = dz [+ maxpool routing of dpool] masked by the ReLU (recomputed from y,
+//       or read from the saved output when the ReLU followed a residual add),
+//   dgamma = sum g*xhat, dbeta = sum g,  dy = A*g + B*y + C  (fp64 coefficients).
 #include "common.h"
 #include "../../include/stfunet.h"
 #include "reduce.h"
@@ -27,80 +33,103 @@ STF_DEV void load_affine(const float* p, int c, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-int tiles_for(long units) {
-  long t = (units + NT - 1) / NT;
-  return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
+int tiles_per_group(long units_per_group, int groups) {
+  long t = (units_per_group + NT - 1) / NT;
+  const long cap = (1024 + groups - 1) / groups;
+  if (t > cap) t = cap;
+  if (t < 1) t = 1;
+  return (int)t;
 }
 
 // ------------------------------------------------------------------ finalize
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int tiles, int C, int M,
+// stats: [G][T][2][C] with the first S rows of every group folded.  One thread
+// per channel walks the groups in order so running stats see G sequential updates.
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int S, int T, int G, int C, long Mg,
                                    const float* gamma, const float* beta, float mom, float eps,
                                    float* rm, float* rv, float* mean, float* invstd, float* scale,
                                    float* shift) {
-  __shared__ double red[2][4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C && stats)
-    for (int t = grp; t < tiles; t += 4) {
-      s1 += stats[(size_t)t * 2 * C + c];
-      s2 += stats[(size_t)t * 2 * C + C + c];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float run_m = rm ? rm[c] : 0.f, run_v = rv ? rv[c] : 1.f;
+  for (int g = 0; g < G; ++g) {
+    double mu, var;
+    if (!stats) {                        // eval mode: running statistics, no update
+      mu = run_m;
+      var = run_v;
+    } else {
+      double s1 = 0.0, s2 = 0.0;
+      const float* base = stats + (size_t)g * T * 2 * C;
+      for (int t = 0; t < S; ++t) { s1 += base[(size_t)t * 2 * C + c]; s2 += base[(size_t)t * 2 * C + C + c]; }
+      mu = s1 / Mg;
+      var = s2 / Mg - mu * mu;
+      if (var < 0) var = 0;
     }
-  red[0][grp][cl] = s1;
-  red[1][grp][cl] = s2;
-  __syncthreads();
-  if (grp != 0 || c >= C) return;
-  double mu, var;
-  if (!stats) {                       // eval mode: normalise with the running statistics
-    mu = rm[c];
-    var = rv[c];
-  } else {
-    for (int g = 1; g < 4; ++g) { s1 += red[0][g][cl]; s2 += red[1][g][cl]; }
-    mu = s1 / M;
-    var = s2 / M - mu * mu;
-    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * inv;
+    mean[g * C + c] = (float)mu;
+    invstd[g * C + c] = inv;
+    scale[g * C + c] = sc;
+    shift[g * C + c] = beta[c] - (float)mu * sc;
+    if (rm && stats) {
+      run_m = (1.f - mom) * run_m + mom * (float)mu;
+      const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
+      run_v = (1.f - mom) * run_v + mom * (float)unb;
+    }
   }
-  const float inv = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = gamma[c] * inv;
-  mean[c] = (float)mu;
-  invstd[c] = inv;
-  scale[c] = sc;
-  shift[c] = beta[c] - (float)mu * sc;
-  if (rm && stats) {
-    rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
-    const double unb = M > 1 ? var * M / (M - 1) : var;
-    rv[c] = (1.f - mom) * rv[c] + mom * (float)unb;
-  }
+  if (rm && stats) { rm[c] = run_m; rv[c] = run_v; }
 }
 
-// ------------------------------------------------------------------ apply (+ pool)
+// ------------------------------------------------------------------ apply
+// res_mode 0: none, 1: + res tensor, 2: + (res*rscale[g] + rshift[g])
 template <bool POOL>
-__global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, int N, int H, int W, int C,
+__global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, int H, int W, int C, long Mg,
                               const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+                              int res_mode, const uint16_t* __restrict__ res, int rcs,
+                              const float* __restrict__ rscale, const float* __restrict__ rshift,
                               uint16_t* __restrict__ out, int ocs, uint16_t* __restrict__ pooled) {
   const int CG = C / 8;
-  const long units = POOL ? (long)N * (H / 2) * (W / 2) * CG : (long)N * H * W * CG;
+  const long units = POOL ? N * (H / 2) * (W / 2) * CG : N * H * W * CG;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
     const int cg = (int)(u % CG);
     const long pix = u / CG;
-    float sc[8], sh[8];
-    load_affine(scale, cg * 8, sc);
-    load_affine(shift, cg * 8, sh);
     if (!POOL) {
-      float v[8];
+      const int g = (int)(pix / Mg);
+      float sc[8], sh[8], v[8];
+      load_affine(scale + (size_t)g * C, cg * 8, sc);
+      load_affine(shift + (size_t)g * C, cg * 8, sh);
       unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { v[j] = v[j] * sc[j] + sh[j]; if (relu) v[j] = fmaxf(v[j], 0.f); }
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+      if (res_mode) {
+        float r[8];
+        unpack8(*reinterpret_cast<const uint4*>(res + pix * rcs + cg * 8), r);
+        if (res_mode == 2) {
+          float rs[8], rh[8];
+          load_affine(rscale + (size_t)g * C, cg * 8, rs);
+          load_affine(rshift + (size_t)g * C, cg * 8, rh);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = r[j] * rs[j] + rh[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += r[j];
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
       *reinterpret_cast<uint4*>(out + pix * ocs + cg * 8) = pack8(v);
     } else {
       const int Wp = W / 2, Hp = H / 2;
-      const int n = (int)(pix / ((long)Hp * Wp));
-      const int rem = (int)(pix - (long)n * Hp * Wp);
+      const long n = pix / ((long)Hp * Wp);
+      const int rem = (int)(pix - n * Hp * Wp);
       const int py = rem / Wp, px = rem - py * Wp;
-      float mx[8];
+      const int g = (int)(n * H * W / Mg);
+      float sc[8], sh[8], mx[8];
+      load_affine(scale + (size_t)g * C, cg * 8, sc);
+      load_affine(shift + (size_t)g * C, cg * 8, sh);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const long p = ((long)n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
+        const long p = (n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
         float v[8];
         unpack8(*reinterpret_cast<const uint4*>(y + p * ycs + cg * 8), v);
 #pragma unroll
@@ -118,33 +147,42 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, int N, in
 }
 
 // ------------------------------------------------------------------ backward reduce
+// mask_mode 0: none, 1: relu(y*scale+shift) > 0, 2: mask_src > 0
 template <bool POOL>
 __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, const uint16_t* __restrict__ dpool,
-                                     const uint16_t* __restrict__ y, int ycs, int N, int H, int W, int C,
-                                     const float* __restrict__ scale, const float* __restrict__ shift,
-                                     const float* __restrict__ mean, const float* __restrict__ invstd, int relu,
+                                     const uint16_t* __restrict__ y, int ycs, long N, int H, int W, int C, int G,
+                                     int tpg, const float* __restrict__ scale, const float* __restrict__ shift,
+                                     const float* __restrict__ mean, const float* __restrict__ invstd,
+                                     int mask_mode, const uint16_t* __restrict__ msrc, int mcs,
                                      uint16_t* __restrict__ g_out, float* __restrict__ partial) {
   __shared__ float red[NT][17];
   const int CG = C / 8;
-  const long units = POOL ? (long)N * (H / 2) * (W / 2) * CG : (long)N * H * W * CG;
-  const long gt = blockIdx.x * (long)NT + threadIdx.x;
-  const int cg = (int)(gt % CG);                 // constant: total threads is a multiple of CG
+  const int g = blockIdx.x / tpg, tile = blockIdx.x - g * tpg;
+  const long Ng = N / G;
+  const long ppg = POOL ? Ng * (H / 2) * (W / 2) : Ng * H * W;            // pixels (or windows) per group
+  const long upg = ppg * CG;
+  const long gt = (long)tile * NT + threadIdx.x;
+  const int cg = (int)(gt % CG);                 // constant: tpg*NT is a multiple of CG
   float sc[8], sh[8], mu[8], is[8];
-  load_affine(scale, cg * 8, sc);
-  load_affine(shift, cg * 8, sh);
-  load_affine(mean, cg * 8, mu);
-  load_affine(invstd, cg * 8, is);
+  load_affine(scale + (size_t)g * C, cg * 8, sc);
+  load_affine(shift + (size_t)g * C, cg * 8, sh);
+  load_affine(mean + (size_t)g * C, cg * 8, mu);
+  load_affine(invstd + (size_t)g * C, cg * 8, is);
   float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long u = gt; u < units; u += (long)gridDim.x * NT) {
-    const long pix = u / CG;
+  for (long u = gt; u < upg; u += (long)tpg * NT) {
+    const long pix = u / CG + g * ppg;
     if (!POOL) {
       float v[8], d[8];
       unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), v);
       unpack8(*reinterpret_cast<const uint4*>(dz + pix * dzcs + cg * 8), d);
+      float mk[8];
+      if (mask_mode == 2) unpack8(*reinterpret_cast<const uint4*>(msrc + pix * mcs + cg * 8), mk);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float z = v[j] * sc[j] + sh[j];
-        const float gj = (relu && !(z > 0.f)) ? 0.f : d[j];
+        bool keep = true;
+        if (mask_mode == 1) keep = v[j] * sc[j] + sh[j] > 0.f;
+        else if (mask_mode == 2) keep = mk[j] > 0.f;
+        const float gj = keep ? d[j] : 0.f;
         d[j] = gj;
         sg[j] += gj;
         sgx[j] += gj * (v[j] - mu[j]) * is[j];
@@ -152,19 +190,19 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
       *reinterpret_cast<uint4*>(g_out + pix * C + cg * 8) = pack8(d);
     } else {
       const int Wp = W / 2, Hp = H / 2;
-      const int n = (int)(pix / ((long)Hp * Wp));
-      const int rem = (int)(pix - (long)n * Hp * Wp);
+      const long n = pix / ((long)Hp * Wp);
+      const int rem = (int)(pix - n * Hp * Wp);
       const int py = rem / Wp, px = rem - py * Wp;
       float v[4][8], a[4][8];
       long p[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        p[d] = ((long)n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
+        p[d] = (n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
         unpack8(*reinterpret_cast<const uint4*>(y + p[d] * ycs + cg * 8), v[d]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float t = v[d][j] * sc[j] + sh[j];
-          if (relu) t = fmaxf(t, 0.f);
+          if (mask_mode == 1) t = fmaxf(t, 0.f);
           a[d][j] = round_bf(t);
         }
       }
@@ -189,8 +227,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float t = gd[j] + (am[j] == d ? dp[j] : 0.f);
-          const float z = v[d][j] * sc[j] + sh[j];
-          if (relu && !(z > 0.f)) t = 0.f;
+          if (mask_mode == 1 && !(v[d][j] * sc[j] + sh[j] > 0.f)) t = 0.f;
           gd[j] = t;
           sg[j] += t;
           sgx[j] += t * (v[d][j] - mu[j]) * is[j];
@@ -203,61 +240,66 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
   for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += NT) {
-    const int g = c / 8, j = c - g * 8;
+    const int gg = c / 8, j = c - gg * 8;
     float a = 0.f, b = 0.f;
-    for (int t = g; t < NT; t += CG) { a += red[t][j]; b += red[t][8 + j]; }
+    for (int t = gg; t < NT; t += CG) { a += red[t][j]; b += red[t][8 + j]; }
     partial[(size_t)blockIdx.x * 2 * C + c] = a;
     partial[(size_t)blockIdx.x * 2 * C + C + c] = b;
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int tiles, int C, int M,
+// partial: [G][T][2][C] (first S rows per group folded).  coef: [G][3][C];
+// dgamma/dbeta are summed over groups (one BatchNorm module, G calls).
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int S, int T, int G, int C, long Mg,
                                        const float* gamma, const float* mean, const float* invstd,
                                        float* dgamma, float* dbeta, float* coef) {
-  __shared__ double red[2][4][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < C)
-    for (int t = grp; t < tiles; t += 4) {
-      s1 += partial[(size_t)t * 2 * C + c];
-      s2 += partial[(size_t)t * 2 * C + C + c];
-    }
-  red[0][grp][cl] = s1;
-  red[1][grp][cl] = s2;
-  __syncthreads();
-  if (grp != 0 || c >= C) return;
-  for (int g = 1; g < 4; ++g) { s1 += red[0][g][cl]; s2 += red[1][g][cl]; }
-  if (dgamma) dgamma[c] = (float)s2;
-  if (dbeta) dbeta[c] = (float)s1;
-  const double A = (double)gamma[c] * invstd[c];
-  const double B = -A * invstd[c] * s2 / M;
-  const double Cc = -A * s1 / M + A * invstd[c] * mean[c] * s2 / M;
-  coef[c] = (float)A;
-  coef[C + c] = (float)B;
-  coef[2 * C + c] = (float)Cc;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double dg = 0.0, db = 0.0;
+  for (int g = 0; g < G; ++g) {
+    double s1 = 0.0, s2 = 0.0;
+    const float* base = partial + (size_t)g * T * 2 * C;
+    for (int t = 0; t < S; ++t) { s1 += base[(size_t)t * 2 * C + c]; s2 += base[(size_t)t * 2 * C + C + c]; }
+    dg += s2;
+    db += s1;
+    const double is = invstd[g * C + c];
+    const double A = (double)gamma[c] * is;
+    const double B = -A * is * s2 / Mg;
+    const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
+    coef[(size_t)g * 3 * C + c] = (float)A;
+    coef[(size_t)g * 3 * C + C + c] = (float)B;
+    coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
+  }
+  if (dgamma) dgamma[c] = (float)dg;
+  if (dbeta) dbeta[c] = (float)db;
 }
 
-__global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restrict__ y, int ycs,
-                                    long M, int C, const float* __restrict__ coef, uint16_t* dy,
+__global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restrict__ y, int ycs, long M, int C,
+                                    long Mg, const float* __restrict__ coef, uint16_t* dy, int dycs,
                                     float* __restrict__ bias_partial) {
   __shared__ float red[NT][9];
   const int CG = C / 8;
   const long units = M * CG;
   const long gt = blockIdx.x * (long)NT + threadIdx.x;
   const int cg = (int)(gt % CG);
-  float A[8], B[8], Cc[8], sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  load_affine(coef, cg * 8, A);
-  load_affine(coef + C, cg * 8, B);
-  load_affine(coef + 2 * C, cg * 8, Cc);
+  float sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int cur_g = -1;
+  float A[8], B[8], Cc[8];
   for (long u = gt; u < units; u += (long)gridDim.x * NT) {
     const long pix = u / CG;
+    const int grp = (int)(pix / Mg);
+    if (grp != cur_g) {
+      cur_g = grp;
+      load_affine(coef + (size_t)grp * 3 * C, cg * 8, A);
+      load_affine(coef + (size_t)grp * 3 * C + C, cg * 8, B);
+      load_affine(coef + (size_t)grp * 3 * C + 2 * C, cg * 8, Cc);
+    }
     float gv[8], yv[8];
     unpack8(*reinterpret_cast<const uint4*>(g + pix * C + cg * 8), gv);
     unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), yv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { gv[j] = A[j] * gv[j] + B[j] * yv[j] + Cc[j]; sb[j] += gv[j]; }
-    *reinterpret_cast<uint4*>(dy + pix * C + cg * 8) = pack8(gv);
+    *reinterpret_cast<uint4*>(dy + pix * dycs + cg * 8) = pack8(gv);
   }
   if (!bias_partial) return;
 #pragma unroll
@@ -273,7 +315,7 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restric
 
 }  // namespace
 
-// sum over tiles of partial[t][C] -> out[C] (fixed order); shared with misc.hip
+// sum over tiles of partial[t][C] -> out[C] (fixed order); shared with misc.hip / loss.hip
 __global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -284,78 +326,103 @@ __global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles
 
 static bool cg_ok(int C) { return C % 8 == 0 && NT % (C / 8) == 0; }
 
-extern "C" int stf_bn_finalize(float* stats, int tiles, int C, int M, const float* gamma, const float* beta,
-                               float momentum, float eps, float* running_mean, float* running_var, float* mean,
-                               float* invstd, float* scale, float* shift, stf_stream_t stream) {
-  if (stats) tiles = stf::colsum_stage1(stats, tiles, 2L * C, (hipStream_t)stream);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, stats, tiles,
-                     C, M, gamma, beta, momentum, eps, running_mean, running_var, mean, invstd, scale, shift);
+extern "C" int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64_t M, const float* gamma,
+                               const float* beta, float momentum, float eps, float* running_mean,
+                               float* running_var, float* mean, float* invstd, float* scale, float* shift,
+                               stf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (groups < 1 || M % groups) return STF_EINVAL;
+  const int S = stats ? stf::colsum_stage1(stats, tiles, 2L * C, s, groups) : 0;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats, S, tiles, groups, C,
+                     (long)(M / groups), gamma, beta, momentum, eps, running_mean, running_var, mean, invstd,
+                     scale, shift);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int C, const float* scale,
-                          const float* shift, int relu, void* out, int out_cstride, void* pooled,
-                          stf_stream_t stream) {
-  if (C % 8 || y_cstride % 8 || out_cstride % 8 || (pooled && ((H | W) & 1))) return STF_EINVAL;
-  const long units = pooled ? (long)N * (H / 2) * (W / 2) * (C / 8) : (long)N * H * W * (C / 8);
+extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int C, int groups,
+                          const float* scale, const float* shift, int relu, const void* res, int res_cstride,
+                          const float* res_scale, const float* res_shift, void* out, int out_cstride,
+                          void* pooled, stf_stream_t stream) {
+  if (C % 8 || y_cstride % 8 || out_cstride % 8 || (pooled && ((H | W) & 1)) || groups < 1 || N % groups)
+    return STF_EINVAL;
+  if (res && (res_cstride % 8 || pooled)) return STF_EINVAL;
+  const int res_mode = res ? (res_scale ? 2 : 1) : 0;
+  const long M = (long)N * H * W;
+  const long units = pooled ? (long)N * (H / 2) * (W / 2) * (C / 8) : M * (C / 8);
   long blocks = (units + NT - 1) / NT;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) return 0;
   hipStream_t s = (hipStream_t)stream;
+  const long Mg = M / groups;
   if (pooled)
-    hipLaunchKernelGGL(bn_act_kernel<true>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, N, H, W,
-                       C, scale, shift, relu, (uint16_t*)out, out_cstride, (uint16_t*)pooled);
+    hipLaunchKernelGGL(bn_act_kernel<true>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (long)N, H,
+                       W, C, Mg, scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
+                       (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled);
   else
-    hipLaunchKernelGGL(bn_act_kernel<false>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, N, H,
-                       W, C, scale, shift, relu, (uint16_t*)out, out_cstride, (uint16_t*)nullptr);
+    hipLaunchKernelGGL(bn_act_kernel<false>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (long)N,
+                       H, W, C, Mg, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
+                       res_shift, (uint16_t*)out, out_cstride, (uint16_t*)nullptr);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int stf_bn_bwd_tiles(int N, int H, int W, int C, int pooled) {
-  const long units = pooled ? (long)N * (H / 2) * (W / 2) * (C / 8) : (long)N * H * W * (C / 8);
-  return tiles_for(units);
+extern "C" int stf_bn_bwd_tiles(int N, int H, int W, int C, int groups, int pooled) {
+  const long Ng = (long)N / groups;
+  const long upg = pooled ? Ng * (H / 2) * (W / 2) * (C / 8) : Ng * H * W * (C / 8);
+  return tiles_per_group(upg, groups);
 }
 
 extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const void* y, int y_cstride,
-                                 int N, int H, int W, int C, const float* scale, const float* shift,
-                                 const float* mean, const float* invstd, int relu, void* g_out, float* partial,
-                                 stf_stream_t stream) {
-  if (!cg_ok(C) || y_cstride % 8 || (dz && dz_cstride % 8)) return STF_EINVAL;
+                                 int N, int H, int W, int C, int groups, const float* scale, const float* shift,
+                                 const float* mean, const float* invstd, int mask_mode, const void* mask_src,
+                                 int mask_cstride, void* g_out, float* partial, stf_stream_t stream) {
+  if (!cg_ok(C) || y_cstride % 8 || (dz && dz_cstride % 8) || groups < 1 || N % groups) return STF_EINVAL;
   if (!dz && !dpool) return STF_EINVAL;
-  if (dpool && ((H | W) & 1)) return STF_EINVAL;
-  const int tiles = stf_bn_bwd_tiles(N, H, W, C, dpool != nullptr);
+  if (dpool && (((H | W) & 1) || mask_mode == 2)) return STF_EINVAL;
+  if (mask_mode == 2 && (!mask_src || mask_cstride % 8)) return STF_EINVAL;
+  const int tpg = stf_bn_bwd_tiles(N, H, W, C, groups, dpool != nullptr);
   hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(tpg * groups);
   if (dpool)
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride,
-                       (const uint16_t*)dpool, (const uint16_t*)y, y_cstride, N, H, W, C, scale, shift, mean,
-                       invstd, relu, (uint16_t*)g_out, partial);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride,
+                       (const uint16_t*)dpool, (const uint16_t*)y, y_cstride, (long)N, H, W, C, groups, tpg, scale,
+                       shift, mean, invstd, mask_mode, (const uint16_t*)mask_src, mask_cstride, (uint16_t*)g_out,
+                       partial);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride,
-                       (const uint16_t*)nullptr, (const uint16_t*)y, y_cstride, N, H, W, C, scale, shift, mean,
-                       invstd, relu, (uint16_t*)g_out, partial);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, grid, dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride,
+                       (const uint16_t*)nullptr, (const uint16_t*)y, y_cstride, (long)N, H, W, C, groups, tpg,
+                       scale, shift, mean, invstd, mask_mode, (const uint16_t*)mask_src, mask_cstride,
+                       (uint16_t*)g_out, partial);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int C, int M, const float* gamma,
+extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C, int64_t M, const float* gamma,
                                    const float* mean, const float* invstd, float* dgamma, float* dbeta, float* coef,
                                    stf_stream_t stream) {
-  tiles = stf::colsum_stage1(partial, tiles, 2L * C, (hipStream_t)stream);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, (hipStream_t)stream, partial,
-                     tiles, C, M, gamma, mean, invstd, dgamma, dbeta, coef);
+  hipStream_t s = (hipStream_t)stream;
+  if (groups < 1 || M % groups) return STF_EINVAL;
+  const int S = stf::colsum_stage1(partial, tiles, 2L * C, s, groups);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, S, tiles, groups, C,
+                     (long)(M / groups), gamma, mean, invstd, dgamma, dbeta, coef);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int M, int C, const float* coef,
-                                void* dy, float* bias_partial, float* dbias, stf_stream_t stream) {
-  if (!cg_ok(C) || y_cstride % 8) return STF_EINVAL;
-  const int tiles = tiles_for((long)M * (C / 8));
+extern "C" int stf_bn_bwd_apply_tiles(int64_t M, int C) {
+  long t = (M * (C / 8) + NT - 1) / NT;
+  return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
+}
+
+extern "C" int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int64_t M, int C, int groups,
+                                const float* coef, void* dy, int dy_cstride, float* bias_partial, float* dbias,
+                                stf_stream_t stream) {
+  if (!cg_ok(C) || y_cstride % 8 || dy_cstride % 8 || groups < 1 || M % groups) return STF_EINVAL;
+  const int tiles = stf_bn_bwd_apply_tiles(M, C);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, (const uint16_t*)y,
-                     y_cstride, (long)M, C, coef, (uint16_t*)dy, bias_partial);
+                     y_cstride, (long)M, C, (long)(M / groups), coef, (uint16_t*)dy, dy_cstride, bias_partial);
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
     const int S = stf::colsum_stage1(bias_partial, tiles, C, s);

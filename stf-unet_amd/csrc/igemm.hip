@@ -24,11 +24,17 @@ struct Geo {
   const uint16_t* src; const uint16_t* wgt; uint16_t* dst;
   const float* bias; float* stats;
   int N, Hs, Ws, Cs, scs, Hd, Wd, R, S, st, pad, M, K, Nout, dcs;
+  int Mg, tpg;          // rows per statistics group, M tiles per group
+  int accumulate;
+  // LSTM cell epilogue (Nout = 4*Ch, column 4c+q = gate q of hidden channel c)
+  const float* c_prev; float* c_out; uint16_t* h_out; int hcs; float* gates;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
 
-template <int BM, int BN, int WM, int WN, bool SMALLC, bool TRANS, bool SCATTER>
+STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int BM, int BN, int WM, int WN, bool SMALLC, bool TRANS, bool SCATTER, int EPI>
 __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;     // wave tile (pixels x channels)
   constexpr int TM = WTM / 16, TN = WTN / 16;     // 16x16 fragments per wave
@@ -42,7 +48,10 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // M tiles never straddle a statistics group: block x = (group, tile within group)
+  const int grp = blockIdx.x / a.tpg, gtile = blockIdx.x - grp * a.tpg;
+  const int m0 = grp * a.Mg + gtile * BM, n0 = blockIdx.y * BN;
+  const int m_end = min(m0 + BM, min((grp + 1) * a.Mg, a.M));
   const int kc = tid & 3;                 // this thread's 16-B chunk within a 64-B row
 
   // per-row gather state for the im2col rows this thread stages
@@ -51,7 +60,7 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
 #pragma unroll
   for (int i = 0; i < CHA; ++i) {
     const int m = m0 + (tid >> 2) + i * (NT / 4);
-    rok[i] = m < a.M;
+    rok[i] = m < m_end;
     const int mm = rok[i] ? m : 0;
     const int hw = a.Hd * a.Wd;
     const int n = mm / hw, rem = mm - n * hw;
@@ -173,29 +182,48 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wm * WTM + i * 16 + fr;
+      if (!(m < m_end && nb < a.Nout)) continue;
+      if (EPI == 1) {
+        // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
+        const int ch = nb >> 2, Ch = a.Nout >> 2;
+        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
+        const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+        const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
+        const float c = gf * cp + gi * gg;
+        a.c_out[(size_t)m * Ch + ch] = c;
+        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanhf(c));
+        *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+        continue;
+      }
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = round_bf(acc[i][j][r] + bv[r]);
-      if (m < a.M && nb < a.Nout) {
-        uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        size_t off;
-        if (SCATTER) {
-          const int blk = nb / Cout, co = nb - blk * Cout;
-          const int hw = a.Hd * a.Wd;
-          const int n = m / hw, rem = m - n * hw;
-          const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
-          const int yo = 2 * yd + (blk >> 1), xo = 2 * xd + (blk & 1);
-          off = ((size_t)(n * 2 * a.Hd + yo) * (2 * a.Wd) + xo) * a.dcs + co;
-        } else {
-          off = (size_t)m * a.dcs + nb;
-        }
-        *reinterpret_cast<uint2*>(a.dst + off) = pk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
+      size_t off;
+      if (SCATTER) {
+        const int blk = nb / Cout, co = nb - blk * Cout;
+        const int hw = a.Hd * a.Wd;
+        const int n = m / hw, rem = m - n * hw;
+        const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+        const int yo = 2 * yd + (blk >> 1), xo = 2 * xd + (blk & 1);
+        off = ((size_t)(n * 2 * a.Hd + yo) * (2 * a.Wd) + xo) * a.dcs + co;
+      } else {
+        off = (size_t)m * a.dcs + nb;
       }
+      if (a.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(a.dst + off);
+        v[0] += __uint_as_float(old.x << 16);
+        v[1] += __uint_as_float(old.x & 0xffff0000u);
+        v[2] += __uint_as_float(old.y << 16);
+        v[3] += __uint_as_float(old.y & 0xffff0000u);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = round_bf(v[r]);
+      *reinterpret_cast<uint2*>(a.dst + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
     }
   }
-  if (a.stats == nullptr) return;
+  if (EPI != 0 || a.stats == nullptr) return;
   // reduce over the 16 pixels held by lanes with equal fk, then over the WM waves
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -231,18 +259,19 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, hipStream_t s) {
-  dim3 grid((g.M + BM - 1) / BM, (g.Nout + BN - 1) / BN), block(NT);
-#define STF_L(SC, TR, SCA) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA>), grid, block, 0, s, g)
-  if (scatter) { if (smallc) STF_L(true, false, true); else STF_L(false, false, true); }
-  else if (trans) { if (smallc) STF_L(true, true, false); else STF_L(false, true, false); }
-  else { if (smallc) STF_L(true, false, false); else STF_L(false, false, false); }
+int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, hipStream_t s) {
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(NT);
+#define STF_L(SC, TR, SCA, E) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA, E>), grid, block, 0, s, g)
+  if (lstm) { if (smallc) return STF_EINVAL; STF_L(false, false, false, 1); }
+  else if (scatter) { if (smallc) STF_L(true, false, true, 0); else STF_L(false, false, true, 0); }
+  else if (trans) { if (smallc) STF_L(true, true, false, 0); else STF_L(false, true, false, 0); }
+  else { if (smallc) STF_L(true, false, false, 0); else STF_L(false, false, false, 0); }
 #undef STF_L
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-int pick_mtile(const stf_igemm_args* a) { return a->Nout <= 64 ? 256 : 128; }
+int pick_mtile(const stf_igemm_args* a) { return (a->Nout <= 64 && !a->lstm) ? 256 : 128; }
 
 }  // namespace
 
@@ -261,8 +290,20 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   g.Hd = c.Hd; g.Wd = c.Wd; g.R = c.R; g.S = c.S; g.st = c.stride; g.pad = c.pad;
   g.M = c.N * c.Hd * c.Wd; g.K = c.R * c.S * c.Cs; g.Nout = a->Nout; g.dcs = a->dst_cstride;
   if (g.M <= 0) return 0;
+  const int bm = pick_mtile(a);
+  g.Mg = a->group_rows > 0 ? a->group_rows : g.M;
+  if (g.M % g.Mg) return STF_EINVAL;
+  g.tpg = (g.Mg + bm - 1) / bm;
+  g.accumulate = a->accumulate;
+  g.c_prev = nullptr; g.c_out = nullptr; g.h_out = nullptr; g.hcs = 0; g.gates = nullptr;
+  if (a->lstm) {
+    if (a->scatter2x2 || c.transposed || a->Nout % 4 || !a->lstm->c_out || !a->lstm->h_out || !a->lstm->gates)
+      return STF_EINVAL;
+    g.c_prev = a->lstm->c_prev; g.c_out = a->lstm->c_out; g.h_out = (uint16_t*)a->lstm->h_out;
+    g.hcs = a->lstm->h_cstride; g.gates = a->lstm->gates;
+  }
   const bool smallc = (c.Cs % BK) != 0;
   hipStream_t s = (hipStream_t)stream;
-  if (pick_mtile(a) == 256) return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, s);
-  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, s);
+  if (bm == 256) return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
+  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
 }

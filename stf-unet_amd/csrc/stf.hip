@@ -1,0 +1,272 @@
+// STF-LSTM-UNet specific kernels (src/stf_lstm_unet.py):
+//   * input packing: [B, T(+P), C, H, W] fp32 -> t-major NHWC bf16 [T*B, H, W, Cpad]
+//     with the PK maps appended as channels of every frame (:146-156,172-174)
+//   * MaxPool2d(3, 2, 1) forward / backward (ResNet stem, :110,180)
+//   * nn.LSTM weight packing into one gate-interleaved [W_ih | W_hh] GEMM operand,
+//     the cell backward (BPTT) and the gradient unpacking (:124-127,214-236)
+//   * bilinear (align_corners=True) resize of the PK maps into the PK-fusion
+//     concat buffers (:189-200)
+#include "common.h"
+#include "../../include/stfunet.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+long grid_for(long units, long cap) {
+  long b = (units + NT - 1) / NT;
+  return b < 1 ? 1 : (b > cap ? cap : b);
+}
+
+// out[(t*B + b)][y][x][c]: c < C -> x[b][t][c], C <= c < C+P -> x[b][T + (c-C)][0], else 0
+__global__ void pack_sequence_kernel(const float* __restrict__ x, int B, int Ttot, int C, int H, int W, int T, int P,
+                                     int Cpad, uint16_t* __restrict__ out) {
+  const long HW = (long)H * W, Pix = (long)T * B * HW;
+  const int CG = Cpad / 8;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < Pix * CG; u += (long)gridDim.x * NT) {
+    const long pix = u % Pix;
+    const int cg = (int)(u / Pix);
+    const long img = pix / HW, hw = pix - img * HW;
+    const int t = (int)(img / B), b = (int)(img - (long)t * B);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      float val = 0.f;
+      if (c < C) val = x[(((long)b * Ttot + t) * C + c) * HW + hw];
+      else if (c < C + P) val = x[(((long)b * Ttot + T + (c - C)) * C) * HW + hw];
+      v[j] = val;
+    }
+    *reinterpret_cast<uint4*>(out + pix * Cpad + cg * 8) = pack8(v);
+  }
+}
+
+// MaxPool2d(k=3, s=2, p=1); first maximum in row-major window order (torch CPU)
+__global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo,
+                                    uint16_t* __restrict__ out) {
+  const int CG = C / 8;
+  const long units = (long)N * Ho * Wo * CG;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long p = u / CG;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int oy = rem / Wo, ox = rem - oy * Wo;
+    float mx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx[j] = -INFINITY;
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = 2 * oy - 1 + dy;
+      if (iy < 0 || iy >= H) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ix = 2 * ox - 1 + dx;
+        if (ix < 0 || ix >= W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + iy) * W + ix) * C + cg * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx[j] = v[j] > mx[j] ? v[j] : mx[j];
+      }
+    }
+    *reinterpret_cast<uint4*>(out + p * C + cg * 8) = pack8(mx);
+  }
+}
+
+// gather form of the backward: every input pixel sums dout over the (<= 4)
+// windows whose recomputed argmax is this pixel -- no atomics, deterministic
+__global__ void maxpool3_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dout, int N, int H,
+                                    int W, int C, int Ho, int Wo, uint16_t* __restrict__ dx) {
+  const int CG = C / 8;
+  const long units = (long)N * H * W * CG;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long p = u / CG;
+    const int n = (int)(p / ((long)H * W));
+    const int rem = (int)(p - (long)n * H * W);
+    const int iy = rem / W, ix = rem - iy * W;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // windows containing iy: 2*oy-1 <= iy <= 2*oy+1  <=>  iy/2 <= oy <= (iy+1)/2
+    for (int oy = iy / 2; oy <= min(Ho - 1, (iy + 1) / 2); ++oy) {
+      for (int ox = ix / 2; ox <= min(Wo - 1, (ix + 1) / 2); ++ox) {
+        float best[8];
+        int arg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = -1; }
+        for (int dy = 0; dy < 3; ++dy) {
+          const int yy = 2 * oy - 1 + dy;
+          if (yy < 0 || yy >= H) continue;
+          for (int dxw = 0; dxw < 3; ++dxw) {
+            const int xx = 2 * ox - 1 + dxw;
+            if (xx < 0 || xx >= W) continue;
+            float v[8];
+            unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + yy) * W + xx) * C + cg * 8), v);
+            const int id = yy * W + xx;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (v[j] > best[j] || arg[j] < 0) { best[j] = v[j]; arg[j] = id; }
+          }
+        }
+        float d[8];
+        unpack8(*reinterpret_cast<const uint4*>(dout + (((long)n * Ho + oy) * Wo + ox) * C + cg * 8), d);
+        const int me = iy * W + ix;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) if (arg[j] == me) acc[j] += d[j];
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + p * C + cg * 8) = pack8(acc);
+  }
+}
+
+// W_ih, W_hh [4C][C] (torch rows: gate q block q*C..) -> wcat [4C][2C] with row 4c+q,
+// wcat_t [2C][4C] (its transpose, for the input gradient), bias[4c+q] = b_ih + b_hh
+__global__ void lstm_pack_kernel(const float* __restrict__ wih, const float* __restrict__ whh,
+                                 const float* __restrict__ bih, const float* __restrict__ bhh, int C,
+                                 bf16* __restrict__ wcat, bf16* __restrict__ wcat_t, float* __restrict__ bias) {
+  const long total = 8L * C * C;
+  for (long o = blockIdx.x * (long)NT + threadIdx.x; o < total; o += (long)gridDim.x * NT) {
+    const int row = (int)(o / (2 * C)), col = (int)(o - (long)row * 2 * C);   // row = 4c + q
+    const int c = row >> 2, q = row & 3;
+    const int src_row = q * C + c;
+    const float v = col < C ? wih[(long)src_row * C + col] : whh[(long)src_row * C + col - C];
+    wcat[o] = f2bf(v);
+    wcat_t[(long)col * 4 * C + row] = f2bf(v);
+    if (col == 0) bias[row] = (bih ? bih[src_row] : 0.f) + (bhh ? bhh[src_row] : 0.f);
+  }
+}
+
+__global__ void lstm_unpack_grad_kernel(const float* __restrict__ dwcat, const float* __restrict__ dbias, int C,
+                                        float* __restrict__ dwih, float* __restrict__ dwhh,
+                                        float* __restrict__ dbih, float* __restrict__ dbhh) {
+  const long total = 8L * C * C;
+  for (long o = blockIdx.x * (long)NT + threadIdx.x; o < total; o += (long)gridDim.x * NT) {
+    const int row = (int)(o / (2 * C)), col = (int)(o - (long)row * 2 * C);
+    const int c = row >> 2, q = row & 3;
+    const int dst_row = q * C + c;
+    if (col < C) dwih[(long)dst_row * C + col] = dwcat[o];
+    else dwhh[(long)dst_row * C + col - C] = dwcat[o];
+    if (col == 0) {
+      if (dbih) dbih[dst_row] = dbias[row];
+      if (dbhh) dbhh[dst_row] = dbias[row];
+    }
+  }
+}
+
+// BPTT cell step for (m, c):  tc = tanh(c_t)
+//   dc = dh*o*(1-tc^2) + dc_next;  do = dh*tc*o(1-o);  di = dc*g*i(1-i);
+//   dg = dc*i*(1-g^2);  df = dc*c_prev*f(1-f);  dc_prev = dc*f
+__global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
+                                     const float* __restrict__ cprev, const uint16_t* __restrict__ dh, int dhcs,
+                                     const float* dc_in, float* dc_out, bf16* __restrict__ dgates, long M, int C) {
+  const long total = M * C;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < total; u += (long)gridDim.x * NT) {
+    const long m = u / C;
+    const int c = (int)(u - m * C);
+    const float4 gv = *reinterpret_cast<const float4*>(gates + m * 4 * C + 4 * c);
+    const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
+    const float ct = cst[u];
+    const float tc = tanhf(ct);
+    const float h = bf2f(reinterpret_cast<const bf16*>(dh)[m * dhcs + c]);
+    float dc = h * go * (1.f - tc * tc) + (dc_in ? dc_in[u] : 0.f);
+    const float cp = cprev ? cprev[u] : 0.f;
+    const float d_o = h * tc * go * (1.f - go);
+    const float d_i = dc * gg * gi * (1.f - gi);
+    const float d_g = dc * gi * (1.f - gg * gg);
+    const float d_f = dc * cp * gf * (1.f - gf);
+    dc_out[u] = dc * gf;
+    const uint2 pk = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
+    *reinterpret_cast<uint2*>(dgates + m * 4 * C + 4 * c) = pk;
+  }
+}
+
+// bilinear, align_corners=True (F.interpolate) of pk [B][P][H][W] to (h, w), written
+// for every time step t into dst[(t*B + b)][y][x][coff + p] (bf16, stride dcs)
+__global__ void pk_resize_kernel(const float* __restrict__ x, int B, int Ttot, int T, int P, int H, int W, int h,
+                                 int w, uint16_t* __restrict__ dst, int dcs, int coff) {
+  const long total = (long)T * B * h * w * P;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < total; u += (long)gridDim.x * NT) {
+    const int p = (int)(u % P);
+    const long pix = u / P;
+    const int xo = (int)(pix % w);
+    const long r1 = pix / w;
+    const int yo = (int)(r1 % h);
+    const long img = r1 / h;
+    const int b = (int)(img % B);
+    const float sy = h > 1 ? (float)(H - 1) / (h - 1) : 0.f, sx = w > 1 ? (float)(W - 1) / (w - 1) : 0.f;
+    const float fy = yo * sy, fx = xo * sx;
+    const int y0 = min((int)fy, H - 1), x0 = min((int)fx, W - 1);
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const float ly = fy - y0, lx = fx - x0;
+    const float* src = x + ((long)b * Ttot + T + p) * H * W;      // frame channel 0 of PK slot p
+    const float v = (1.f - ly) * ((1.f - lx) * src[(long)y0 * W + x0] + lx * src[(long)y0 * W + x1]) +
+                    ly * ((1.f - lx) * src[(long)y1 * W + x0] + lx * src[(long)y1 * W + x1]);
+    reinterpret_cast<bf16*>(dst)[pix * dcs + coff + p] = f2bf(v);
+  }
+}
+
+}  // namespace
+
+extern "C" int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int T, int P, int Cpad,
+                                 void* out, stf_stream_t stream) {
+  if (Cpad % 8 || Cpad < C + P || Ttot < T + P || (P && C != 1)) return STF_EINVAL;
+  const long units = (long)T * B * H * W * (Cpad / 8);
+  hipLaunchKernelGGL(pack_sequence_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream, x, B,
+                     Ttot, C, H, W, T, P, Cpad, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, stf_stream_t stream) {
+  if (C % 8) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long units = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)x, N, H, W, C, Ho, Wo, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_maxpool3s2_bwd(const void* x, const void* dout, int N, int H, int W, int C, void* dx,
+                                  stf_stream_t stream) {
+  if (C % 8) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long units = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)x, (const uint16_t*)dout, N, H, W, C, Ho, Wo, (uint16_t*)dx);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, int C,
+                             void* wcat, void* wcat_t, float* bias, stf_stream_t stream) {
+  if (C % 8) return STF_EINVAL;
+  hipLaunchKernelGGL(lstm_pack_kernel, dim3(grid_for(8L * C * C, 4096)), dim3(NT), 0, (hipStream_t)stream, w_ih,
+                     w_hh, b_ih, b_hh, C, (bf16*)wcat, (bf16*)wcat_t, bias);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih, float* dw_hh,
+                                    float* db_ih, float* db_hh, stf_stream_t stream) {
+  hipLaunchKernelGGL(lstm_unpack_grad_kernel, dim3(grid_for(8L * C * C, 4096)), dim3(NT), 0, (hipStream_t)stream,
+                     dwcat, dbias, C, dw_ih, dw_hh, db_ih, db_hh);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_lstm_cell_bwd(const float* gates, const float* c_t, const float* c_prev, const void* dh,
+                                 int dh_cstride, const float* dc_in, float* dc_out, void* dgates, int64_t M, int C,
+                                 stf_stream_t stream) {
+  if (C % 2) return STF_EINVAL;
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(grid_for((long)M * C, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     gates, c_t, c_prev, (const uint16_t*)dh, dh_cstride, dc_in, dc_out, (bf16*)dgates, (long)M, C);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int H, int W, int h, int w, void* dst,
+                             int dst_cstride, int coff, stf_stream_t stream) {
+  const long total = (long)T * B * h * w * P;
+  hipLaunchKernelGGL(pk_resize_kernel, dim3(grid_for(total, 8192)), dim3(NT), 0, (hipStream_t)stream, x, B, Ttot,
+                     T, P, H, W, h, w, (uint16_t*)dst, dst_cstride, coff);
+  STF_CHECK_LAUNCH();
+  return 0;
+}

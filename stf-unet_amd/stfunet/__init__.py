@@ -6,6 +6,7 @@ output and ``state_dict`` keys) whose forward/backward run hand-written HIP
 kernels through the C ABI in ``include/stfunet.h``.
 """
 from . import _lib  # noqa: F401
+from .stf_lstm_unet import STFLSTMUNet  # noqa: F401
 from .unet import UNet  # noqa: F401
 
-__all__ = ["UNet"]
+__all__ = ["STFLSTMUNet", "UNet"]

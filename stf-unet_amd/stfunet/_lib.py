@@ -23,9 +23,14 @@ class ConvGeom(ctypes.Structure):
                                      "stride", "pad", "transposed")]
 
 
+class LstmEpi(ctypes.Structure):
+    _fields_ = [("c_prev", P), ("c_out", P), ("h_out", P), ("h_cstride", c_int), ("gates", P)]
+
+
 class IgemmArgs(ctypes.Structure):
     _fields_ = [("g", ConvGeom), ("src", P), ("wgt", P), ("Nout", c_int), ("dst", P),
-                ("dst_cstride", c_int), ("bias", P), ("stats", P), ("scatter2x2", c_int)]
+                ("dst_cstride", c_int), ("bias", P), ("stats", P), ("scatter2x2", c_int),
+                ("group_rows", c_int), ("accumulate", c_int), ("lstm", ctypes.POINTER(LstmEpi))]
 
 
 class WgradArgs(ctypes.Structure):
@@ -41,13 +46,15 @@ _SIGS = {
     "stf_wgrad": (c_int, [ctypes.POINTER(WgradArgs), P]),
     "stf_wgrad_reduce": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_channel_sum": (c_int, [P, c_int, c_int, c_int, P, P, P]),
-    "stf_bn_finalize": (c_int, [P, c_int, c_int, c_int, P, P, c_float, c_float, P, P, P, P, P, P, P]),
-    "stf_bn_act": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P, P]),
-    "stf_bn_bwd_tiles": (c_int, [c_int, c_int, c_int, c_int, c_int]),
-    "stf_bn_bwd_reduce": (c_int, [P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P,
-                                  P, P]),
-    "stf_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_int, P, P, P, P, P, P, P]),
-    "stf_bn_bwd_apply": (c_int, [P, P, c_int, c_int, c_int, P, P, P, P, P]),
+    "stf_bn_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, c_float, c_float, P, P, P, P, P, P, P]),
+    "stf_bn_act": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P, P, P, c_int, P,
+                           P]),
+    "stf_bn_bwd_tiles": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "stf_bn_bwd_reduce": (c_int, [P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P,
+                                  c_int, P, P, P]),
+    "stf_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, P, P, P, P, P]),
+    "stf_bn_bwd_apply_tiles": (c_int, [c_int64, c_int]),
+    "stf_bn_bwd_apply": (c_int, [P, P, c_int, c_int64, c_int, c_int, P, P, c_int, P, P, P]),
     "stf_head_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "stf_head_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P, P, P]),
     "stf_head_tiles": (c_int, [c_int, c_int, c_int, c_int]),
@@ -58,6 +65,13 @@ _SIGS = {
                           P]),
     "stf_pack_input": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_maxpool3s2_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
+    "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "stf_lstm_pack": (c_int, [P, P, P, P, c_int, P, P, P, P]),
+    "stf_lstm_unpack_grad": (c_int, [P, P, c_int, P, P, P, P, P]),
+    "stf_lstm_cell_bwd": (c_int, [P, P, P, P, c_int, P, P, P, c_int64, c_int, P]),
+    "stf_pk_resize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "stf_error_string": (ctypes.c_char_p, [c_int]),
     "stf_abi_version": (c_int, []),
 }

@@ -123,26 +123,29 @@ def _geom(src: Feat, Hd, Wd, R, S, stride, pad, transposed):
 
 
 def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, bias=None,
-          want_stats=False, scatter2x2=False):
-    """Launch stf_igemm; returns the per-tile stats tensor (or None) and tile count."""
+          want_stats=False, scatter2x2=False, groups=1, accumulate=False, lstm=None):
+    """Launch stf_igemm; returns the per-tile stats tensor (or None) and tiles per group."""
     src.check()
     dst.check()
     Hd, Wd = (dst.H // 2, dst.W // 2) if scatter2x2 else (dst.H, dst.W)
-    assert dst.N == src.N
-    assert dst.C == (nout // 4 if scatter2x2 else nout)
+    assert dst.N == src.N and src.N % groups == 0
+    if lstm is None:
+        assert dst.C == (nout // 4 if scatter2x2 else nout)
     assert wgt.dtype == BF16 and wgt.numel() == nout * R * S * src.C
     if transposed:
         assert stride in (1, 2)
     else:
         # every gathered tap must stay inside (or be zero padding of) the source
         assert (Hd - 1) * stride - pad + R - 1 <= src.H - 1 + pad
+    M = src.N * Hd * Wd
     a = IgemmArgs(_geom(src, Hd, Wd, R, S, stride, pad, transposed), src.ptr(), _p(wgt), nout, dst.ptr(),
-                  dst.cs, _p(bias), None, int(scatter2x2))
+                  dst.cs, _p(bias), None, int(scatter2x2), M // groups if groups > 1 else 0, int(accumulate),
+                  ctypes.pointer(lstm) if lstm is not None else None)
     stats, tiles = None, 0
     if want_stats:
         mt = _lib.load().stf_igemm_mtile(ctypes.byref(a))
-        tiles = (src.N * Hd * Wd + mt - 1) // mt
-        stats = torch.empty(tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
+        tiles = (M // groups + mt - 1) // mt
+        stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
         a.stats = _p(stats)
     t = TIMER
     ev = t.begin() if t is not None else None
@@ -153,13 +156,19 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     return stats, tiles
 
 
-def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad):
+def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False):
     """Conv2d input gradient: stride 1 runs as a forward gather over flipped taps
-    (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather."""
+    (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather.
+    ``accumulate``: dx += gradient (residual / multi-consumer tensors)."""
     if stride == 1 and 2 * pad == R - 1 and R == S:
-        igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad)
+        igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate)
     else:
-        igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True)
+        igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True, accumulate=accumulate)
+
+
+def rows(f: Feat, n0, n):
+    """Images [n0, n0+n) of a Feat (same H, W, channel slice)."""
+    return Feat(f.buf[n0 * f.H * f.W * f.cs:], n, f.H, f.W, f.C, f.cs, f.off)
 
 
 def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
@@ -192,55 +201,78 @@ def channel_sum(x: Feat, out):
 
 # ------------------------------------------------------------------ BatchNorm
 class BNState:
-    """Per-forward BatchNorm quantities kept for backward."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "M")
+    """Per-forward BatchNorm quantities ([groups][C] each) kept for backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups")
 
-    def __init__(self, C, device, M):
-        t = torch.empty(4 * C, dtype=torch.float32, device=device)
-        self.mean, self.invstd, self.scale, self.shift = t.view(4, C).unbind(0)
+    def __init__(self, C, device, M, groups=1):
+        t = torch.empty(4, groups, C, dtype=torch.float32, device=device)
+        self.mean, self.invstd, self.scale, self.shift = t.unbind(0)
         self.M = M
+        self.groups = groups
+
+    @staticmethod
+    def identity(C, device):
+        st = BNState(C, device, 0, 1)
+        st.mean.zero_()
+        st.invstd.fill_(1.0)
+        st.scale.fill_(1.0)
+        st.shift.zero_()
+        return st
 
 
-def bn_finalize(stats, tiles, bn, M, training):
+def bn_finalize(stats, tiles, bn, M, training, groups=1):
     """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats."""
     C = bn.num_features
-    st = BNState(C, bn.weight.device, M)
+    st = BNState(C, bn.weight.device, M, groups)
     mom = 0.1 if bn.momentum is None else bn.momentum
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    call("stf_bn_finalize", _p(stats) if training else None, tiles, C, M, _p(bn.weight.detach()),
+    call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, _p(bn.weight.detach()),
          _p(bn.bias.detach()), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
          _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
          stream())
     if training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
+        bn.num_batches_tracked.add_(groups)
     return st
 
 
-def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None):
+def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None, res: Feat = None,
+           res_st: BNState = None):
+    """out = act(BN(y) [+ res | + BN_res(res)]) (+ 2x2 max pool into ``pooled``)."""
     y.check()
     out.check()
     assert (y.N, y.H, y.W, y.C) == (out.N, out.H, out.W, out.C)
     if pooled is not None:
         pooled.check()
         assert pooled.cs == pooled.C and pooled.off == 0 and (pooled.H, pooled.W) == (y.H // 2, y.W // 2)
-    call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, _p(st.scale), _p(st.shift), int(relu), out.ptr(),
-         out.cs, pooled.ptr() if pooled is not None else None, stream())
+    if res is not None:
+        res.check()
+        assert (res.N, res.H, res.W, res.C) == (y.N, y.H, y.W, y.C)
+    call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, st.groups, _p(st.scale), _p(st.shift), int(relu),
+         res.ptr() if res is not None else None, res.cs if res is not None else 0,
+         _p(res_st.scale) if res_st is not None else None, _p(res_st.shift) if res_st is not None else None,
+         out.ptr(), out.cs, pooled.ptr() if pooled is not None else None, stream())
 
 
 def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool: Feat = None, relu=True,
-                dbias=None):
-    """Gradient of relu(BN(y)) [+ maxpool] w.r.t. y; returns dy as a dense Feat.
+                dbias=None, mask: Feat = None, out: Feat = None, keep_g=False):
+    """Gradient of act(BN(y)) [+ maxpool] w.r.t. y; returns dy as a Feat.
 
     ``dz``: grad w.r.t. the BN(+ReLU) output (may be a concat slice);
-    ``dpool``: grad w.r.t. its 2x2 max-pooled output.  dgamma/dbeta/dbias are
-    fp32 views in the flat gradient buffer (dbias: bias of the producing conv).
+    ``dpool``: grad w.r.t. its 2x2 max-pooled output; ``mask``: take the ReLU
+    mask from this saved output instead of recomputing it (ReLU after a
+    residual add).  ``relu=False`` and no mask: plain BN backward.
+    dgamma/dbeta/dbias: fp32 views in the flat gradient buffer (dbias = bias of
+    the producing conv).  ``out``: optional destination Feat for dy.
+    ``keep_g``: return (dy, g) with g = the masked incoming gradient (the
+    residual-shortcut gradient of a block whose ReLU follows the add).
     """
     y.check()
     C = y.C
     dev = y.buf.device
-    tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, int(dpool is not None))
-    part = torch.empty(tiles * 2 * C, dtype=torch.float32, device=dev)
+    G = st.groups
+    tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, G, int(dpool is not None))
+    part = torch.empty(G * tiles * 2 * C, dtype=torch.float32, device=dev)
     g = new_feat(y.N, y.H, y.W, C, dev)
     if dz is not None:
         dz.check()
@@ -248,22 +280,34 @@ def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool:
     if dpool is not None:
         dpool.check()
         assert dpool.cs == C and dpool.off == 0 and (dpool.H, dpool.W) == (y.H // 2, y.W // 2)
+    mode = 2 if mask is not None else (1 if relu else 0)
+    if mask is not None:
+        mask.check()
     call("stf_bn_bwd_reduce", dz.ptr() if dz is not None else None, dz.cs if dz is not None else 0,
-         dpool.ptr() if dpool is not None else None, y.ptr(), y.cs, y.N, y.H, y.W, C, _p(st.scale),
-         _p(st.shift), _p(st.mean), _p(st.invstd), int(relu), g.ptr(), _p(part), stream())
-    return bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias)
+         dpool.ptr() if dpool is not None else None, y.ptr(), y.cs, y.N, y.H, y.W, C, G, _p(st.scale),
+         _p(st.shift), _p(st.mean), _p(st.invstd), mode, mask.ptr() if mask is not None else None,
+         mask.cs if mask is not None else 0, g.ptr(), _p(part), stream())
+    if keep_g and out is None:
+        out = new_feat(y.N, y.H, y.W, C, dev)
+    dy = bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=out)
+    return (dy, g) if keep_g else dy
 
 
-def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None):
+def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None,
+                             out: Feat = None):
     C = y.C
     dev = y.buf.device
-    coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-    call("stf_bn_bwd_finalize", _p(part), tiles, C, y.M, _p(bn.weight.detach()), _p(st.mean),
+    G = st.groups
+    coef = torch.empty(G * 3 * C, dtype=torch.float32, device=dev)
+    call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, _p(bn.weight.detach()), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     bpart = None
     if dbias is not None:
-        btiles = min(1024, max(1, (y.M * (C // 8) + 255) // 256))
-        bpart = torch.empty(btiles * C, dtype=torch.float32, device=dev)
-    call("stf_bn_bwd_apply", g.ptr(), y.ptr(), y.cs, y.M, C, _p(coef), g.ptr(), _p(bpart), _p(dbias),
-         stream())
-    return g
+        bpart = torch.empty(_lib.load().stf_bn_bwd_apply_tiles(y.M, C) * C, dtype=torch.float32, device=dev)
+    dst = out if out is not None else g
+    if out is not None:
+        out.check()
+        assert (out.N, out.H, out.W, out.C) == (y.N, y.H, y.W, C)
+    call("stf_bn_bwd_apply", g.ptr(), y.ptr(), y.cs, y.M, C, G, _p(coef), dst.ptr(), dst.cs, _p(bpart),
+         _p(dbias), stream())
+    return dst

@@ -1,0 +1,505 @@
+"""Drop-in ``STFLSTMUNet`` (reference ``src/stf_lstm_unet.py:89-256``) on gfx950 kernels.
+
+Surface kept: ``STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8,
+use_pk_maps=False, pk_channels=3)``, ``forward(x, pk_maps=None) -> {"out": logits}``
+with x [B, T(+P), C, H, W] and logits at H/2 x W/2 (the reference's output size,
+SURVEY.md section 0), the module tree and therefore all ``state_dict`` keys:
+``conv1``/``bn1``/``layer1..4`` (torchvision ResNet-34 names, BasicBlock
+``conv1,bn1,conv2,bn2,downsample``), ``pk_fusion1..4``, ``lstm1..4`` (nn.LSTM
+parameters), ``decoder4..2`` (``up``, ``fusion``, ``res_conv.conv_block``),
+``upconv1``, ``final_res``, ``final``.
+
+Schedule (all NHWC bf16, fp32 statistics; ``STFProgram``):
+  * the T time steps are one batch of T*B images, t-major; every BatchNorm of the
+    encoder keeps per-time-step statistics (groups = T) and advances its running
+    stats T times, as the reference's per-t loop does (:168-186);
+  * stem conv7x7/s2 (+BN+ReLU) -> MaxPool(3,2,1) -> ResNet-34 BasicBlocks with the
+    residual add + ReLU fused into the second BN's apply pass;
+  * each layer's output is written straight into the [x_t | h_{t-1}] buffer of
+    its LSTM; every LSTM step is ONE implicit GEMM (K = 2C, N = 4C gate-interleaved)
+    whose epilogue is the cell update, writing h_t into the next step's buffer
+    and h_T into the decoder's concat buffer (skip "cat" without a copy);
+  * decoder: ConvTranspose2d(3,2,1,1) as a transposed gather into the concat
+    buffer, 1x1 fusion conv, ResidualConvBlock; final 1x1 fused into the head.
+  * backward mirrors it (BPTT = per-step cell kernel + one GEMM; LSTM weight
+    gradients = one GEMM over all T steps).
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib, nhwc
+from ._lib import LstmEpi, call, stream
+from .flat import FlatParams
+from .nhwc import BNState, Feat, _p, new_feat, rows, zeros_feat
+
+
+def _c8(c):
+    return (c + 7) // 8 * 8
+
+
+# ------------------------------------------------------------------ module tree
+class BasicBlock(nn.Module):
+    """torchvision ResNet BasicBlock parameter container (names are the contract)."""
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+
+def _resnet_layer(inplanes, planes, blocks, stride):
+    ds = None
+    if stride != 1 or inplanes != planes:
+        ds = nn.Sequential(nn.Conv2d(inplanes, planes, 1, stride, bias=False), nn.BatchNorm2d(planes))
+    layers = [BasicBlock(inplanes, planes, stride, ds)]
+    layers += [BasicBlock(planes, planes) for _ in range(1, blocks)]
+    return nn.Sequential(*layers)
+
+
+class ResidualConvBlock(nn.Module):
+    """src/stf_lstm_unet.py:7-35 (conv_block 0/1/3/4, optional 1x1 shortcut)."""
+    input_format = "time_sequence"
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.conv_block = nn.Sequential(
+            nn.Conv2d(in_channels, out_channels, 3, padding=1, bias=False), nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True), nn.Conv2d(out_channels, out_channels, 3, padding=1, bias=False),
+            nn.BatchNorm2d(out_channels))
+        self.shortcut = nn.Sequential()
+        if in_channels != out_channels:
+            self.shortcut = nn.Sequential(nn.Conv2d(in_channels, out_channels, 1, bias=False),
+                                          nn.BatchNorm2d(out_channels))
+        self.relu = nn.ReLU(inplace=True)
+
+
+class DecoderBlock(nn.Module):
+    """src/stf_lstm_unet.py:38-68."""
+
+    def __init__(self, in_channels, skip_channels, out_channels):
+        super().__init__()
+        self.up = nn.ConvTranspose2d(in_channels, out_channels, kernel_size=3, stride=2, padding=1,
+                                     output_padding=1)
+        self.fusion = nn.Conv2d(out_channels + skip_channels, out_channels, kernel_size=1)
+        self.res_conv = ResidualConvBlock(out_channels, out_channels)
+
+
+class _S:
+    pass
+
+
+# ------------------------------------------------------------------ block programs
+class ResBlockProgram:
+    """BasicBlock / ResidualConvBlock: out = relu(bn2(conv2(relu(bn1(conv1 x)))) + sc(x))."""
+
+    def __init__(self, conv1, bn1, conv2, bn2, sc_conv=None, sc_bn=None):
+        self.conv1, self.bn1, self.conv2, self.bn2 = conv1, bn1, conv2, bn2
+        self.sc_conv, self.sc_bn = sc_conv, sc_bn
+        self.stride = conv1.stride[0]
+        self.cout = conv1.out_channels
+
+    def forward(self, src: Feat, out: Feat, training, groups):
+        dev, C, st = src.buf.device, self.cout, self.stride
+        Ho, Wo = (src.H - 1) // st + 1, (src.W - 1) // st + 1
+        s = _S()
+        s.src, s.out = src, out
+        y1 = new_feat(src.N, Ho, Wo, C, dev)
+        stats, tiles = nhwc.igemm(src, nhwc.pack_weight(self.conv1.weight, 0, src.C), C, y1, 3, 3, st, 1,
+                                  want_stats=training, groups=groups)
+        s.bn1 = nhwc.bn_finalize(stats, tiles, self.bn1, y1.M, training, groups)
+        a1 = new_feat(src.N, Ho, Wo, C, dev)
+        nhwc.bn_act(y1, s.bn1, a1)
+        y2 = new_feat(src.N, Ho, Wo, C, dev)
+        stats, tiles = nhwc.igemm(a1, nhwc.pack_weight(self.conv2.weight, 0, C), C, y2, 3, 3, 1, 1,
+                                  want_stats=training, groups=groups)
+        s.bn2 = nhwc.bn_finalize(stats, tiles, self.bn2, y2.M, training, groups)
+        s.yd = s.bnd = None
+        if self.sc_conv is not None:
+            yd = new_feat(src.N, Ho, Wo, C, dev)
+            stats, tiles = nhwc.igemm(src, nhwc.pack_weight(self.sc_conv.weight, 0, src.C), C, yd, 1, 1, st, 0,
+                                      want_stats=training, groups=groups)
+            s.bnd = nhwc.bn_finalize(stats, tiles, self.sc_bn, yd.M, training, groups)
+            s.yd = yd
+            nhwc.bn_act(y2, s.bn2, out, res=yd, res_st=s.bnd)
+        else:
+            nhwc.bn_act(y2, s.bn2, out, res=src)
+        s.y1, s.a1, s.y2 = y1, a1, y2
+        return s
+
+    def backward(self, s, gv, dout: Feat = None, g: Feat = None, dsrc: Feat = None, need_dsrc=True):
+        """``dout``: grad w.r.t. the block output (masked here by out > 0), or
+        ``g``: already-masked grad (the head fused the final ReLU).  ``dsrc``:
+        destination that the input gradient is accumulated into (None: new)."""
+        src = s.src
+        if g is None:
+            dy2, g = nhwc.bn_backward(s.y2, s.bn2, self.bn2, gv(self.bn2.weight), gv(self.bn2.bias), dz=dout,
+                                      mask=s.out, keep_g=True)
+        else:
+            dy2 = nhwc.bn_backward(s.y2, s.bn2, self.bn2, gv(self.bn2.weight), gv(self.bn2.bias), dz=g,
+                                   relu=False, out=new_feat(g.N, g.H, g.W, g.C, g.buf.device))
+        nhwc.wgrad(dy2, s.a1, 3, 3, 1, 1, gv(self.conv2.weight))
+        da1 = new_feat(s.a1.N, s.a1.H, s.a1.W, self.cout, s.a1.buf.device)
+        nhwc.conv_dgrad(dy2, self.conv2.weight, da1, 3, 3, 1, 1)
+        del dy2
+        dy1 = nhwc.bn_backward(s.y1, s.bn1, self.bn1, gv(self.bn1.weight), gv(self.bn1.bias), dz=da1)
+        del da1
+        nhwc.wgrad(dy1, src, 3, 3, self.stride, 1, gv(self.conv1.weight))
+        if self.sc_conv is None:
+            # identity shortcut: d_src = g + dgrad(conv1)
+            if dsrc is not None:
+                raise NotImplementedError("identity-shortcut blocks produce their input gradient in place")
+            nhwc.conv_dgrad(dy1, self.conv1.weight, g, 3, 3, self.stride, 1, accumulate=True)
+            return g
+        dyd = nhwc.bn_backward(s.yd, s.bnd, self.sc_bn, gv(self.sc_bn.weight), gv(self.sc_bn.bias), dz=g,
+                               relu=False)
+        nhwc.wgrad(dyd, src, 1, 1, self.stride, 0, gv(self.sc_conv.weight))
+        if not need_dsrc:
+            return None
+        acc = dsrc is not None
+        if dsrc is None:
+            dsrc = new_feat(src.N, src.H, src.W, src.C, src.buf.device)
+        nhwc.conv_dgrad(dyd, self.sc_conv.weight, dsrc, 1, 1, self.stride, 0, accumulate=acc)
+        nhwc.conv_dgrad(dy1, self.conv1.weight, dsrc, 3, 3, self.stride, 1, accumulate=True)
+        return dsrc
+
+
+# ------------------------------------------------------------------ program
+class STFProgram:
+    def __init__(self, m):
+        self.m = m
+        self.flat = FlatParams(m)
+        self.grad_ready_hook = None
+        self.layers = []
+        for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
+            progs = []
+            for blk in layer:
+                ds = blk.downsample
+                progs.append(ResBlockProgram(blk.conv1, blk.bn1, blk.conv2, blk.bn2,
+                                             ds[0] if ds is not None else None, ds[1] if ds is not None else None))
+            self.layers.append(progs)
+        self.decoders = [m.decoder4, m.decoder3, m.decoder2]
+        self.dec_res = [ResBlockProgram(d.res_conv.conv_block[0], d.res_conv.conv_block[1],
+                                        d.res_conv.conv_block[3], d.res_conv.conv_block[4])
+                        for d in self.decoders]
+        fr = m.final_res
+        self.final_res = ResBlockProgram(fr.conv_block[0], fr.conv_block[1], fr.conv_block[3], fr.conv_block[4])
+        self.lstms = [m.lstm1, m.lstm2, m.lstm3, m.lstm4]
+
+    def _done(self, module):
+        if self.grad_ready_hook is not None:
+            first = next(module.parameters())
+            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x, training, need_bwd):
+        m = self.m
+        dev = x.device
+        B, Ttot, Cf, H, W = x.shape
+        P = m.pk_channels if m.use_pk_maps else 0
+        T = Ttot - P
+        assert T >= 1 and H % 32 == 0 and W % 32 == 0, "STFLSTMUNet needs H, W divisible by 32"
+        x = x.contiguous().float()
+        S = _S()
+        S.B, S.T, S.P, S.H, S.W = B, T, P, H, W
+        N = T * B
+        cpad = _c8(Cf + P)
+        xin = new_feat(N, H, W, cpad, dev)
+        call("stf_pack_sequence", _p(x), B, Ttot, Cf, H, W, T, P, cpad, xin.ptr(), stream())
+        # ---- stem
+        h2, w2 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y0 = new_feat(N, h2, w2, 64, dev)
+        stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(m.conv1.weight, 0, cpad), 64, y0, 7, 7, 2, 3,
+                                  want_stats=training, groups=T)
+        S.bn0 = nhwc.bn_finalize(stats, tiles, m.bn1, y0.M, training, T)
+        a0 = new_feat(N, h2, w2, 64, dev)
+        nhwc.bn_act(y0, S.bn0, a0)
+        h4, w4 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
+        p0 = new_feat(N, h4, w4, 64, dev)
+        call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), stream())
+        S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
+        # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat)
+        S.enc, S.lbuf, S.pkbuf = [], [], []
+        cur = p0
+        for li, progs in enumerate(self.layers):
+            C = progs[0].cout
+            hh, ww = ((cur.H - 1) // progs[0].stride + 1, (cur.W - 1) // progs[0].stride + 1)
+            lbuf = zeros_feat(N, hh, ww, 2 * C, dev)            # [e_t | h_{t-1}], h_{-1} = 0
+            pkb = None
+            if P:
+                pkb = zeros_feat(N, hh, ww, C + 8, dev)
+                call("stf_pk_resize", _p(x), B, Ttot, T, P, H, W, hh, ww, pkb.ptr(), pkb.cs, C, stream())
+            saved = []
+            for bi, bp in enumerate(progs):
+                last = bi == len(progs) - 1
+                if last:
+                    out = pkb.slice(0, C) if P else lbuf.slice(0, C)
+                else:
+                    out = new_feat(N, hh, ww, C, dev)
+                saved.append(bp.forward(cur, out, training, T))
+                cur = out
+            if P:
+                fus = getattr(m, f"pk_fusion{li + 1}")
+                wf = nhwc.pack_weight(fus.weight, 0, C + 8)
+                nhwc.igemm(pkb, wf, C, lbuf.slice(0, C), 1, 1, 1, 0, bias=fus.bias.detach())
+            S.enc.append(saved)
+            S.lbuf.append(lbuf)
+            S.pkbuf.append(pkb)
+        # ---- decoder concat buffers (skip = h_T of the LSTM one scale up)
+        dcat = []
+        for d, lb in zip(self.decoders, (S.lbuf[2], S.lbuf[1], S.lbuf[0])):
+            Cout = d.up.out_channels
+            Cskip = d.fusion.in_channels - Cout
+            dcat.append(new_feat(B, lb.H, lb.W, Cout + Cskip, dev))
+        S.dcat = dcat
+        # ---- per-pixel LSTMs over T
+        S.lstm = []
+        e4f = None
+        for k, lstm in enumerate(self.lstms):
+            lb = S.lbuf[k]
+            C = lstm.hidden_size
+            npix = B * lb.H * lb.W
+            wcat = torch.empty(8 * C * C, dtype=torch.bfloat16, device=dev)
+            wcat_t = torch.empty_like(wcat)
+            bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
+            call("stf_lstm_pack", _p(lstm.weight_ih_l0.detach()), _p(lstm.weight_hh_l0.detach()),
+                 _p(lstm.bias_ih_l0.detach()), _p(lstm.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias),
+                 stream())
+            gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev)
+            cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
+            if k < 3:
+                dc = dcat[2 - k]
+                hT = dc.slice(dc.C - C, C)
+            else:
+                e4f = new_feat(B, lb.H, lb.W, C, dev)
+                hT = e4f
+            for t in range(T):
+                src = rows(lb, t * B, B)
+                hdst = rows(lb, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
+                epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, _p(gates[t]))
+                nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
+            st = _S()
+            st.wcat_t, st.gates, st.c, st.hT = wcat_t, gates, cst, hT
+            S.lstm.append(st)
+        # ---- decoder
+        S.dec = []
+        cur = e4f
+        for i, d in enumerate(self.decoders):
+            cat = dcat[i]
+            Cout = d.up.out_channels
+            nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, cat.slice(0, Cout), 3, 3, 2, 1,
+                       transposed=True, bias=d.up.bias.detach())
+            yf = new_feat(B, cat.H, cat.W, Cout, dev)
+            nhwc.igemm(cat, nhwc.pack_weight(d.fusion.weight, 0, cat.C), Cout, yf, 1, 1, 1, 0,
+                       bias=d.fusion.bias.detach())
+            out = new_feat(B, cat.H, cat.W, Cout, dev)
+            rs = self.dec_res[i].forward(yf, out, training, 1)
+            dsv = _S()
+            dsv.x, dsv.cat, dsv.yf, dsv.res = cur, cat, yf, rs
+            S.dec.append(dsv)
+            cur = out
+        # ---- upconv1 + final_res + final (head)
+        up = m.upconv1
+        u1 = new_feat(B, 2 * cur.H, 2 * cur.W, up.out_channels, dev)
+        nhwc.igemm(cur, nhwc.pack_weight(up.weight, 4), up.out_channels, u1, 3, 3, 2, 1, transposed=True,
+                   bias=up.bias.detach())
+        fr_out = new_feat(B, u1.H, u1.W, up.out_channels, dev)
+        S.fr = self.final_res.forward(u1, fr_out, training, 1)
+        S.d2out, S.u1 = cur, u1
+        K = m.final.out_channels
+        logits = torch.empty(B, K, u1.H, u1.W, dtype=torch.float32, device=dev)
+        S.ident = BNState.identity(fr_out.C, dev)
+        S.head_w = m.final.weight.detach().reshape(K, -1).contiguous()
+        call("stf_head_fwd", fr_out.ptr(), B, u1.H, u1.W, fr_out.C, _p(S.ident.scale), _p(S.ident.shift),
+             _p(S.head_w), _p(m.final.bias.detach()), K, _p(logits), stream())
+        return logits, (S if need_bwd else None)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, S, dlogits):
+        m = self.m
+        gv = self.flat.grad_view
+        dev = dlogits.device
+        dlogits = dlogits.contiguous().float()
+        B, T, P = S.B, S.T, S.P
+        fr_out = S.fr.out
+        K = dlogits.shape[1]
+        C = fr_out.C
+        lib = _lib.load()
+        tiles = lib.stf_head_tiles(B, fr_out.H, fr_out.W, C)
+        g = new_feat(B, fr_out.H, fr_out.W, C, dev)
+        bnp = torch.empty(tiles * 2 * C, dtype=torch.float32, device=dev)
+        hp = torch.empty((tiles + 1) * K * (C + 1), dtype=torch.float32, device=dev)
+        call("stf_head_bwd", _p(dlogits), fr_out.ptr(), B, fr_out.H, fr_out.W, C, _p(S.ident.scale),
+             _p(S.ident.shift), _p(S.ident.mean), _p(S.ident.invstd), _p(S.head_w), K, g.ptr(), _p(bnp), _p(hp),
+             _p(gv(m.final.weight)), _p(gv(m.final.bias)), stream())
+        self._done(m.final)
+        d_u1 = self.final_res.backward(S.fr, gv, g=g)
+        self._done(m.final_res)
+        up = m.upconv1
+        nhwc.wgrad(S.d2out, d_u1, 3, 3, 2, 1, gv(up.weight))
+        nhwc.channel_sum(d_u1, gv(up.bias))
+        dcur = new_feat(B, S.d2out.H, S.d2out.W, S.d2out.C, dev)
+        nhwc.igemm(d_u1, nhwc.pack_weight(up.weight, 3), S.d2out.C, dcur, 3, 3, 2, 1)
+        del d_u1
+        self._done(up)
+        # decoders 2, 3, 4 (reverse of forward order)
+        dhT = [None] * 4
+        for i in (2, 1, 0):
+            d, dsv = self.decoders[i], S.dec[i]
+            Cout = d.up.out_channels
+            d_yf = self.dec_res[i].backward(dsv.res, gv, dout=dcur)
+            nhwc.wgrad(d_yf, dsv.cat, 1, 1, 1, 0, gv(d.fusion.weight))
+            nhwc.channel_sum(d_yf, gv(d.fusion.bias))
+            dcat = new_feat(B, dsv.cat.H, dsv.cat.W, dsv.cat.C, dev)
+            nhwc.conv_dgrad(d_yf, d.fusion.weight, dcat, 1, 1, 1, 0)
+            del d_yf
+            dup = dcat.slice(0, Cout)
+            nhwc.wgrad(dsv.x, dup, 3, 3, 2, 1, gv(d.up.weight))
+            nhwc.channel_sum(dup, gv(d.up.bias))
+            dx = new_feat(B, dsv.x.H, dsv.x.W, dsv.x.C, dev)
+            nhwc.igemm(dup, nhwc.pack_weight(d.up.weight, 3), dsv.x.C, dx, 3, 3, 2, 1)
+            dhT[2 - i] = dcat.slice(Cout, dcat.C - Cout)     # skip of scale 2-i (decoder4 -> scale 3 = idx 2)
+            dcur = dx
+            self._done(d)
+        dhT[3] = dcur                                          # decoder4 input = h_T of lstm4
+        # LSTMs (scale 4 first: its gradient is needed first by the encoder)
+        de = [None] * 4
+        for k in (3, 2, 1, 0):
+            de[k] = self._lstm_backward(S, k, dhT[k], gv)
+            self._done(self.lstms[k])
+        if P:
+            for k in (3, 2, 1, 0):
+                de[k] = self._pk_fusion_backward(S, k, de[k], gv)
+            self._done(m.pk_fusion1)
+        # encoder: layer4 -> layer1; d(layer k-1 output) accumulates into de[k-1]
+        for li in (3, 2, 1, 0):
+            progs, saved = self.layers[li], S.enc[li]
+            dout = de[li]
+            for bi in range(len(progs) - 1, -1, -1):
+                bp, s = progs[bi], saved[bi]
+                if bi == 0:
+                    target = de[li - 1] if li > 0 else None
+                    dout = bp.backward(s, gv, dout=dout, dsrc=target)
+                else:
+                    dout = bp.backward(s, gv, dout=dout)
+            self._done(getattr(m, f"layer{li + 1}"))
+        # stem: maxpool(3,2,1) <- relu(bn1(conv1 x))
+        da0 = new_feat(S.a0.N, S.a0.H, S.a0.W, 64, dev)
+        call("stf_maxpool3s2_bwd", S.a0.ptr(), dout.ptr(), S.a0.N, S.a0.H, S.a0.W, 64, da0.ptr(), stream())
+        dy0 = nhwc.bn_backward(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), dz=da0)
+        cin = m.conv1.in_channels
+        if S.xin.C == cin:
+            nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, gv(m.conv1.weight))
+        else:
+            tmp = torch.empty(64 * S.xin.C * 49, dtype=torch.float32, device=dev)
+            nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp)
+            gv(m.conv1.weight).copy_(tmp.view(64, S.xin.C, 7, 7)[:, :cin])
+
+    def _lstm_backward(self, S, k, dhT: Feat, gv):
+        lstm, st, lb = self.lstms[k], S.lstm[k], S.lbuf[k]
+        B, T = S.B, S.T
+        C = lstm.hidden_size
+        dev = lb.buf.device
+        npix = B * lb.H * lb.W
+        d2 = new_feat(T * B, lb.H, lb.W, 2 * C, dev)           # rows of step t: [de_t | dh_{t-1}]
+        dg = new_feat(T * B, lb.H, lb.W, 4 * C, dev)           # pre-activation gate grads (interleaved)
+        dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
+        for t in range(T - 1, -1, -1):
+            dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
+            dgt = rows(dg, t * B, B)
+            call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None, dh.ptr(),
+                 dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
+            nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
+        dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
+        nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat)
+        dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        nhwc.channel_sum(dg, dbcat)
+        call("stf_lstm_unpack_grad", _p(dwcat), _p(dbcat), C, _p(gv(lstm.weight_ih_l0)), _p(gv(lstm.weight_hh_l0)),
+             _p(gv(lstm.bias_ih_l0)), _p(gv(lstm.bias_hh_l0)), stream())
+        return d2.slice(0, C)                                   # d e_t for every t (stride 2C)
+
+    def _pk_fusion_backward(self, S, k, de: Feat, gv):
+        fus = getattr(self.m, f"pk_fusion{k + 1}")
+        pkb = S.pkbuf[k]
+        C = de.C
+        tmp = torch.empty(C * pkb.C, dtype=torch.float32, device=de.buf.device)
+        nhwc.wgrad(de, pkb, 1, 1, 1, 0, tmp)
+        gv(fus.weight).copy_(tmp.view(C, pkb.C, 1, 1)[:, :fus.in_channels])
+        nhwc.channel_sum(de, gv(fus.bias))
+        dpk = new_feat(pkb.N, pkb.H, pkb.W, pkb.C, de.buf.device)
+        w = torch.zeros(C, pkb.C, 1, 1, dtype=torch.float32, device=de.buf.device)
+        w[:, :fus.in_channels].copy_(fus.weight.detach())
+        nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0)
+        return dpk.slice(0, C)
+
+
+class _STFFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, prog, *params):
+        need_bwd = any(ctx.needs_input_grad[2:])
+        logits, saved = prog.forward(x, prog.m.training, need_bwd)
+        ctx.prog, ctx.saved = prog, saved
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        prog = ctx.prog
+        prog.flat.fresh_grad()
+        prog.backward(ctx.saved, dlogits)
+        ctx.saved = None
+        if prog.grad_ready_hook is not None:
+            prog.grad_ready_hook(0)
+        return (None, None, *prog.flat.grad_views())
+
+
+class STFLSTMUNet(nn.Module):
+    def __init__(self, in_channels=1, num_classes=2, time_steps=8, use_pk_maps=False, pk_channels=3):
+        super().__init__()
+        self.time_steps = time_steps
+        self.use_pk_maps = use_pk_maps
+        self.pk_channels = pk_channels if use_pk_maps else 0
+        actual_in = in_channels + (pk_channels if use_pk_maps else 0)
+        self.conv1 = nn.Conv2d(actual_in, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = _resnet_layer(64, 64, 3, 1)
+        self.layer2 = _resnet_layer(64, 128, 4, 2)
+        self.layer3 = _resnet_layer(128, 256, 6, 2)
+        self.layer4 = _resnet_layer(256, 512, 3, 2)
+        if use_pk_maps:
+            self.pk_fusion1 = nn.Conv2d(64 + pk_channels, 64, kernel_size=1)
+            self.pk_fusion2 = nn.Conv2d(128 + pk_channels, 128, kernel_size=1)
+            self.pk_fusion3 = nn.Conv2d(256 + pk_channels, 256, kernel_size=1)
+            self.pk_fusion4 = nn.Conv2d(512 + pk_channels, 512, kernel_size=1)
+        self.lstm1 = nn.LSTM(64, 64, batch_first=True)
+        self.lstm2 = nn.LSTM(128, 128, batch_first=True)
+        self.lstm3 = nn.LSTM(256, 256, batch_first=True)
+        self.lstm4 = nn.LSTM(512, 512, batch_first=True)
+        self.decoder4 = DecoderBlock(512, 256, 256)
+        self.decoder3 = DecoderBlock(256, 128, 128)
+        self.decoder2 = DecoderBlock(128, 64, 64)
+        self.upconv1 = nn.ConvTranspose2d(64, 32, kernel_size=3, stride=2, padding=1, output_padding=1)
+        self.final_res = ResidualConvBlock(32, 32)
+        self.final = nn.Conv2d(32, num_classes, kernel_size=1)
+        self._program = None
+
+    @property
+    def program(self):
+        if self._program is None:
+            self._program = STFProgram(self)
+        return self._program
+
+    def forward(self, x, pk_maps=None):
+        # pk_maps is ignored, as in the reference (PK maps ride on the T axis, :146-156)
+        if not x.is_cuda:
+            raise RuntimeError("stfunet.STFLSTMUNet runs on the gfx950 HIP kernels only; move the model and "
+                               "input to a ROCm device (no CPU fallback)")
+        prog = self.program
+        prog.flat.ensure()
+        return {"out": _STFFunction.apply(x, prog, *prog.flat.params)}

@@ -57,7 +57,8 @@ def test_library_rejects_bad_shapes_without_launch():
     g = _lib.ConvGeom(1, 8, 8, 12, 12, 8, 8, 3, 3, 1, 1, 0)      # Cs=12: not a multiple of 8
     a = _lib.IgemmArgs(g, None, None, 64, None, 64, None, None, 0)
     assert lib.stf_igemm(ctypes.byref(a), None) == 100001
-    assert lib.stf_bn_act(None, 8, 1, 4, 4, 12, None, None, 1, None, 12, None, None) == 100001
+    assert lib.stf_bn_act(None, 8, 1, 4, 4, 12, 1, None, None, 1, None, 0, None, None, None, 12, None,
+                          None) == 100001
 
 
 def test_preprocess_and_lr_schedule_match_reference():
