@@ -40,10 +40,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="unet", choices=["unet"])
-    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--model", default="unet", choices=["unet", "stf"],
+                    help="unet = BASELINE configs[1] (default); stf = configs[2] (T=8, B=16)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (unet 64, stf 16)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--time-steps", type=int, default=8)
+    ap.add_argument("--pk", action="store_true", help="STF with 3 PK-map channels (configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timer", action="store_true")
@@ -51,27 +53,35 @@ def parse():
 
 
 def cpu_baseline(args):
-    """fp32 oracle (plain PyTorch CPU restatement of src/unet.py + criterion +
-    AdamW) on a bounded sample: B=2 at the same 256x256 frames."""
-    from oracle import loss as o_loss, optim as o_optim, unet as o_unet
+    """fp32 oracle (plain PyTorch CPU restatement of src/unet.py or
+    src/stf_lstm_unet.py + criterion + AdamW) on a bounded sample: B=2 at the
+    same frame size."""
+    from oracle import loss as o_loss, optim as o_optim, stf as o_stf, unet as o_unet
     from oracle.init import canonical_state_dict
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores = max(1, min(cores, 16))
     torch.set_num_threads(cores)
     b = 2
-    sd = canonical_state_dict(o_unet.template_state_dict(args.time_steps, 2, 64), seed=0)
+    g = torch.Generator().manual_seed(1)
+    if args.model == "unet":
+        sd = canonical_state_dict(o_unet.template_state_dict(args.time_steps, 2, 64), seed=0)
+        x = torch.randn(b, args.time_steps, args.size, args.size, generator=g)
+        t = (torch.rand(b, args.size, args.size, generator=g) > 0.8).long()
+        fwd = lambda p: o_unet.forward(p, x, training=True)  # noqa: E731
+    else:
+        sd = canonical_state_dict(o_stf.template_state_dict(use_pk_maps=args.pk), seed=0)
+        x = torch.randn(b, args.time_steps + (3 if args.pk else 0), 1, args.size, args.size, generator=g)
+        t = (torch.rand(b, args.size // 2, args.size // 2, generator=g) > 0.8).long()
+        fwd = lambda p: o_stf.forward(p, x, training=True, use_pk_maps=args.pk)  # noqa: E731
     p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     names = [k for k in p if p[k].requires_grad]
     m = [torch.zeros_like(p[k]) for k in names]
     v = [torch.zeros_like(p[k]) for k in names]
-    g = torch.Generator().manual_seed(1)
-    x = torch.randn(b, args.time_steps, args.size, args.size, generator=g)
-    t = (torch.rand(b, args.size, args.size, generator=g) > 0.8).long()
 
     def step(i):
         for k in names:
             p[k].grad = None
-        loss = o_loss.criterion(o_unet.forward(p, x, training=True)["out"], t)
+        loss = o_loss.criterion(fwd(p)["out"], t)
         loss.backward()
         with torch.no_grad():
             o_optim.adamw_step([p[k] for k in names], [p[k].grad for k in names], m, v, i, lr=1e-3)
@@ -81,10 +91,11 @@ def cpu_baseline(args):
     for i in range(args.cpu_steps):
         step(i + 2)
     dt = (time.perf_counter() - t0) / args.cpu_steps
+    what = (f"UNet(in={args.time_steps}, base_c=64)" if args.model == "unet" else
+            f"STFLSTMUNet(T={args.time_steps}{', PK' if args.pk else ''})")
     return {"value": round(b / dt, 4), "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"oracle fp32 UNet(in={args.time_steps}, base_c=64) train step, batch {b}, "
-                      f"{args.size}x{args.size}, {args.cpu_steps} timed steps after 1 warm-up, "
-                      f"{dt:.3f} s/step"}
+            "sample": f"oracle fp32 {what} train step, batch {b}, {args.size}x{args.size}, "
+                      f"{args.cpu_steps} timed steps after 1 warm-up, {dt:.3f} s/step"}
 
 
 def main():
@@ -103,10 +114,15 @@ def main():
     from stfunet.ddp import GradAllReduce
     from stfunet.optim import AdamW
     from stfunet.synthetic import dce_batch
-    from stfunet.unet import UNet
+    from stfunet import STFLSTMUNet, UNet
 
+    if args.batch is None:
+        args.batch = 64 if args.model == "unet" else 16
     torch.manual_seed(1234)
-    model = UNet(in_channels=args.time_steps, num_classes=2, base_c=64).to(dev)
+    if args.model == "unet":
+        model = UNet(in_channels=args.time_steps, num_classes=2, base_c=64).to(dev)
+    else:
+        model = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=args.time_steps, use_pk_maps=args.pk).to(dev)
     model.train()
     opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
     steps_total = args.warmup + args.steps
@@ -114,8 +130,9 @@ def main():
     ddp = GradAllReduce(model) if world > 1 else None
 
     # synthetic batches resident in HBM before the timed region
-    batches = [dce_batch(args.batch, args.time_steps, args.size, args.size, seed=1000 * rank + i, device=dev)
-               for i in range(2)]
+    half = (args.size // 2, args.size // 2) if args.model == "stf" else None   # STF predicts at H/2
+    batches = [dce_batch(args.batch, args.time_steps, args.size, args.size, seed=1000 * rank + i, device=dev,
+                         pk_channels=3 if args.pk else 0, mask_hw=half) for i in range(2)]
     batches = [(engine.preprocess_input(x, model), t) for x, t in batches]
 
     def train_step(i):
@@ -155,8 +172,12 @@ def main():
     samples = args.batch * world * args.steps
     value = samples / elapsed
     if rank == 0:
-        from oracle.unet import train_flops_per_sample
-        train_gflop = train_flops_per_sample(args.time_steps, 64, args.size, args.size) / 1e9
+        if args.model == "unet":
+            from oracle.unet import train_flops_per_sample
+            train_gflop = train_flops_per_sample(args.time_steps, 64, args.size, args.size) / 1e9
+        else:
+            from oracle.stf import train_flops_per_sample
+            train_gflop = train_flops_per_sample(args.time_steps, args.size, args.size, args.pk) / 1e9
         roof = None
         if "igemm" in kt:
             k = kt["igemm"]
@@ -172,10 +193,15 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
-            "config": {"workload": f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step",
-                       "model": "UNet", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+            "config": {"workload": (f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
+                                    if args.model == "unet" else
+                                    f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
+                                    f"{args.size}x{args.size} train step"),
+                       "model": "UNet" if args.model == "unet" else "STFLSTMUNet",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": args.time_steps, "image": [args.size, args.size],
                        "parallelism": f"dp{world}"},
+            "train_gflop_per_sample": round(train_gflop, 2),
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
             "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
             "roofline": roof,

@@ -201,3 +201,39 @@ def forward(p, x, training=True, use_pk_maps=False, pk_channels=3):
                 enc = k.startswith(("bn1.", "layer"))
                 p[k] += steps if enc else 1
     return {"out": out}
+
+
+def train_flops_per_sample(T=8, H=256, W=256, use_pk_maps=False, pk_channels=3):
+    """Algorithmic FLOPs (2*MAC) of conv/convT/1x1/LSTM GEMMs per sample, x3 for
+    training (SURVEY.md section 8(d) convention; ConvTranspose MACs counted per
+    input pixel: h*w*Cin*Cout*k*k)."""
+    cin = 1 + (pk_channels if use_pk_maps else 0)
+    f = 0.0
+    h, w = H // 2, W // 2
+    f += T * 2 * h * w * 64 * 49 * cin                      # stem
+    h, w = h // 2, w // 2
+    inpl = 64
+    scales = []
+    for planes, blocks, stride in RESNET34_LAYERS:
+        for b in range(blocks):
+            st = stride if b == 0 else 1
+            h2, w2 = h // st, w // st
+            f += T * 2 * h2 * w2 * planes * 9 * inpl            # conv1
+            f += T * 2 * h2 * w2 * planes * 9 * planes          # conv2
+            if b == 0 and (st != 1 or inpl != planes):
+                f += T * 2 * h2 * w2 * planes * inpl            # downsample 1x1
+            h, w, inpl = h2, w2, planes
+        scales.append((planes, h, w))
+    for c, hh, ww in scales:
+        if use_pk_maps:
+            f += T * 2 * hh * ww * c * (c + pk_channels)
+        f += T * 2 * hh * ww * 4 * c * (2 * c)                 # LSTM x- and h-projections
+    for (cin_, hin, win), (cout, hh, ww) in zip(scales[:0:-1], scales[-2::-1]):
+        f += 2 * hin * win * cin_ * cout * 9                    # ConvT k3 s2
+        f += 2 * hh * ww * cout * (2 * cout)                    # 1x1 fusion
+        f += 2 * 2 * hh * ww * cout * 9 * cout                  # ResidualConvBlock
+    c, hh, ww = scales[0]
+    f += 2 * hh * ww * 64 * 32 * 9                              # upconv1
+    f += 2 * 2 * (2 * hh) * (2 * ww) * 32 * 9 * 32              # final_res
+    f += 2 * (2 * hh) * (2 * ww) * 32 * 2                       # final 1x1
+    return 3.0 * f

@@ -169,6 +169,62 @@ class ResBlockProgram:
         return dsrc
 
 
+class LSTMProgram:
+    """nn.LSTM(C, C) over T steps for every pixel, only h_T kept (src/stf_lstm_unet.py:214-242).
+
+    ``lbuf``: [T*B images][h][w][2C] with rows of step t = [x_t | h_{t-1}] (x_t written
+    by the encoder, h_{-1} = 0).  Step t is one implicit GEMM (K = 2C, N = 4C
+    gate-interleaved) with the cell update in its epilogue; h_t lands in step t+1's
+    rows and h_T in ``hT`` (e.g. the decoder's concat slice).
+    """
+
+    def __init__(self, lstm):
+        self.lstm = lstm
+        self.C = lstm.hidden_size
+
+    def forward(self, lbuf: Feat, T, B, hT: Feat):
+        C, dev = self.C, lbuf.buf.device
+        L = self.lstm
+        npix = B * lbuf.H * lbuf.W
+        wcat = torch.empty(8 * C * C, dtype=torch.bfloat16, device=dev)
+        wcat_t = torch.empty_like(wcat)
+        bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        call("stf_lstm_pack", _p(L.weight_ih_l0.detach()), _p(L.weight_hh_l0.detach()), _p(L.bias_ih_l0.detach()),
+             _p(L.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias), stream())
+        gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev)
+        cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
+        for t in range(T):
+            src = rows(lbuf, t * B, B)
+            hdst = rows(lbuf, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
+            epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, _p(gates[t]))
+            nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
+        st = _S()
+        st.lbuf, st.T, st.B, st.wcat_t, st.gates, st.c = lbuf, T, B, wcat_t, gates, cst
+        return st
+
+    def backward(self, st, dhT: Feat, gv):
+        """Returns d x_t for every t as a Feat slice [T*B][h][w][C] (stride 2C)."""
+        L, C, lb, T, B = self.lstm, self.C, st.lbuf, st.T, st.B
+        dev = lb.buf.device
+        npix = B * lb.H * lb.W
+        d2 = new_feat(T * B, lb.H, lb.W, 2 * C, dev)           # rows of step t: [dx_t | dh_{t-1}]
+        dg = new_feat(T * B, lb.H, lb.W, 4 * C, dev)           # pre-activation gate grads (interleaved)
+        dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
+        for t in range(T - 1, -1, -1):
+            dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
+            dgt = rows(dg, t * B, B)
+            call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None, dh.ptr(),
+                 dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
+            nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
+        dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
+        nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat)
+        dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        nhwc.channel_sum(dg, dbcat)
+        call("stf_lstm_unpack_grad", _p(dwcat), _p(dbcat), C, _p(gv(L.weight_ih_l0)), _p(gv(L.weight_hh_l0)),
+             _p(gv(L.bias_ih_l0)), _p(gv(L.bias_hh_l0)), stream())
+        return d2.slice(0, C)
+
+
 # ------------------------------------------------------------------ program
 class STFProgram:
     def __init__(self, m):
@@ -190,6 +246,7 @@ class STFProgram:
         fr = m.final_res
         self.final_res = ResBlockProgram(fr.conv_block[0], fr.conv_block[1], fr.conv_block[3], fr.conv_block[4])
         self.lstms = [m.lstm1, m.lstm2, m.lstm3, m.lstm4]
+        self.lstm_progs = [LSTMProgram(lstm) for lstm in self.lstms]
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
@@ -260,32 +317,15 @@ class STFProgram:
         # ---- per-pixel LSTMs over T
         S.lstm = []
         e4f = None
-        for k, lstm in enumerate(self.lstms):
+        for k, lp in enumerate(self.lstm_progs):
             lb = S.lbuf[k]
-            C = lstm.hidden_size
-            npix = B * lb.H * lb.W
-            wcat = torch.empty(8 * C * C, dtype=torch.bfloat16, device=dev)
-            wcat_t = torch.empty_like(wcat)
-            bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
-            call("stf_lstm_pack", _p(lstm.weight_ih_l0.detach()), _p(lstm.weight_hh_l0.detach()),
-                 _p(lstm.bias_ih_l0.detach()), _p(lstm.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias),
-                 stream())
-            gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev)
-            cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
             if k < 3:
                 dc = dcat[2 - k]
-                hT = dc.slice(dc.C - C, C)
+                hT = dc.slice(dc.C - lp.C, lp.C)
             else:
-                e4f = new_feat(B, lb.H, lb.W, C, dev)
+                e4f = new_feat(B, lb.H, lb.W, lp.C, dev)
                 hT = e4f
-            for t in range(T):
-                src = rows(lb, t * B, B)
-                hdst = rows(lb, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
-                epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, _p(gates[t]))
-                nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
-            st = _S()
-            st.wcat_t, st.gates, st.c, st.hT = wcat_t, gates, cst, hT
-            S.lstm.append(st)
+            S.lstm.append(lp.forward(lb, T, B, hT))
         # ---- decoder
         S.dec = []
         cur = e4f
@@ -370,7 +410,7 @@ class STFProgram:
         # LSTMs (scale 4 first: its gradient is needed first by the encoder)
         de = [None] * 4
         for k in (3, 2, 1, 0):
-            de[k] = self._lstm_backward(S, k, dhT[k], gv)
+            de[k] = self.lstm_progs[k].backward(S.lstm[k], dhT[k], gv)
             self._done(self.lstms[k])
         if P:
             for k in (3, 2, 1, 0):
@@ -399,29 +439,6 @@ class STFProgram:
             tmp = torch.empty(64 * S.xin.C * 49, dtype=torch.float32, device=dev)
             nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp)
             gv(m.conv1.weight).copy_(tmp.view(64, S.xin.C, 7, 7)[:, :cin])
-
-    def _lstm_backward(self, S, k, dhT: Feat, gv):
-        lstm, st, lb = self.lstms[k], S.lstm[k], S.lbuf[k]
-        B, T = S.B, S.T
-        C = lstm.hidden_size
-        dev = lb.buf.device
-        npix = B * lb.H * lb.W
-        d2 = new_feat(T * B, lb.H, lb.W, 2 * C, dev)           # rows of step t: [de_t | dh_{t-1}]
-        dg = new_feat(T * B, lb.H, lb.W, 4 * C, dev)           # pre-activation gate grads (interleaved)
-        dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
-        for t in range(T - 1, -1, -1):
-            dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
-            dgt = rows(dg, t * B, B)
-            call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None, dh.ptr(),
-                 dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
-            nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
-        dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
-        nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat)
-        dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)
-        nhwc.channel_sum(dg, dbcat)
-        call("stf_lstm_unpack_grad", _p(dwcat), _p(dbcat), C, _p(gv(lstm.weight_ih_l0)), _p(gv(lstm.weight_hh_l0)),
-             _p(gv(lstm.bias_ih_l0)), _p(gv(lstm.bias_hh_l0)), stream())
-        return d2.slice(0, C)                                   # d e_t for every t (stride 2C)
 
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
         fus = getattr(self.m, f"pk_fusion{k + 1}")
