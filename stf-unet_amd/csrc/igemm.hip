@@ -14,6 +14,7 @@
 // makes the ds_read_b128 fragment reads conflict-free for all four lane groups.
 #include "common.h"
 #include "../../include/stfunet.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -33,6 +34,106 @@ struct Geo {
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
 
 STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// Shared epilogue: acc[i][j][r] = pixel m0 + wm*WTM + i*16 + (lane&15),
+// channel n0 + wn*WTN + j*16 + (lane>>4)*4 + r.
+template <int BM, int BN, int WM, int WN, bool SCATTER, int EPI>
+STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end, int n0,
+                            int wm, int wn, int tid, char* smem) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
+  const int Cout = SCATTER ? a.Nout / 4 : a.Nout;
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nb = n0 + wn * WTN + j * 16 + fk * 4;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && nb < a.Nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = a.bias[SCATTER ? (nb + r) % Cout : nb + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      if (!(m < m_end && nb < a.Nout)) continue;
+      if (EPI == 1) {
+        // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
+        const int ch = nb >> 2, Ch = a.Nout >> 2;
+        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
+        const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+        const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
+        const float c = gf * cp + gi * gg;
+        a.c_out[(size_t)m * Ch + ch] = c;
+        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanhf(c));
+        *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+        continue;
+      }
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
+      size_t off;
+      if (SCATTER) {
+        const int blk = nb / Cout, co = nb - blk * Cout;
+        const int hw = a.Hd * a.Wd;
+        const int n = m / hw, rem = m - n * hw;
+        const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+        const int yo = 2 * yd + (blk >> 1), xo = 2 * xd + (blk & 1);
+        off = ((size_t)(n * 2 * a.Hd + yo) * (2 * a.Wd) + xo) * a.dcs + co;
+      } else {
+        off = (size_t)m * a.dcs + nb;
+      }
+      if (a.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(a.dst + off);
+        v[0] += __uint_as_float(old.x << 16);
+        v[1] += __uint_as_float(old.x & 0xffff0000u);
+        v[2] += __uint_as_float(old.y << 16);
+        v[3] += __uint_as_float(old.y & 0xffff0000u);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = round_bf(v[r]);
+      *reinterpret_cast<uint2*>(a.dst + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
+    }
+  }
+  if (EPI != 0 || a.stats == nullptr) return;
+  // reduce over the 16 pixels held by lanes with equal fk, then over the WM waves
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
+        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
+      }
+  float* red = reinterpret_cast<float*>(smem);     // [WM][2][BN]
+  __syncthreads();
+  if (fr == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = wn * WTN + j * 16 + fk * 4 + r;
+        red[(wm * 2 + 0) * BN + col] = s1[j][r];
+        red[(wm * 2 + 1) * BN + col] = s2[j][r];
+      }
+  }
+  __syncthreads();
+  for (int col = tid; col < BN; col += NT) {
+    const int n = n0 + col;
+    if (n >= a.Nout) continue;
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { t1 += red[(w * 2) * BN + col]; t2 += red[(w * 2 + 1) * BN + col]; }
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + n] = t1;
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + a.Nout + n] = t2;
+  }
+}
+
 
 template <int BM, int BN, int WM, int WN, bool SMALLC, bool TRANS, bool SCATTER, int EPI>
 __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
@@ -165,102 +266,152 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
     __syncthreads();
   }
 
-  // ------------------------------------------------------------------ epilogue
-  // acc[i][j][r]: pixel m = m0 + wm*WTM + i*16 + fr, channel n = n0 + wn*WTN + j*16 + fk*4 + r
-  const int Cout = SCATTER ? a.Nout / 4 : a.Nout;
-  float s1[TN][4], s2[TN][4];
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA ring variant (Cs % 32 == 0): every 16-B chunk goes global -> LDS with
+// buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write).  The im2col halo
+// and all tails are zero-filled by the buffer range check: an invalid lane gets
+// voffset 0xFFFFFFF0 >= num_records.  One wave-instruction writes 1 KiB = 16
+// rows x 64 B linearly, so the chunk swizzle is applied on the SOURCE side (lane
+// with LDS chunk slot p loads global chunk p ^ swz(row)); the fragment reads use
+// the same involution.  STAGES-deep ring, STAGES-1 K steps in flight across the
+// raw s_barrier; a counted vmcnt retires exactly the stage about to be read.
+template <int BM, int BN, int WM, int WN, bool TRANS, bool SCATTER, int EPI, int STAGES>
+__global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(Geo a, uint32_t src_bytes) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int LA = BM / 64, LB = BN / 64;            // DMA instructions per wave per K step
+  constexpr int STAGE = (BM + BN) * 64;                 // bytes per ring stage
+  constexpr int LDS_MAIN = STAGES * STAGE, LDS_RED = WM * 2 * BN * 4;
+  static_assert(WM * WN == 4 && LA >= 1 && LB >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int grp = blockIdx.x / a.tpg, gtile = blockIdx.x - grp * a.tpg;
+  const int m0 = grp * a.Mg + gtile * BM, n0 = blockIdx.y * BN;
+  const int m_end = min(m0 + BM, min((grp + 1) * a.Mg, a.M));
+  const int sub = lane >> 2, slot = lane & 3;
+
+  const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_wgt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, 0, (uint32_t)a.Nout * a.K * 2, 0x00020000);
+
+  // per-lane gather state: one im2col row per A instruction, one weight row per B instruction
+  int rbase[LA], ry[LA], rx[LA], akc[LA];
+  bool rok[LA];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int nb = n0 + wn * WTN + j * 16 + fk * 4;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.bias && nb < a.Nout) {
+  for (int i = 0; i < LA; ++i) {
+    const int row = wave * (BM / 4) + i * 16 + sub;
+    const int m = m0 + row;
+    rok[i] = m < m_end;
+    const int mm = rok[i] ? m : m0;
+    const int hw = a.Hd * a.Wd;
+    const int n = mm / hw, rem = mm - n * hw;
+    const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+    rbase[i] = n * a.Hs * a.Ws;
+    if (TRANS) { ry[i] = yd + a.pad; rx[i] = xd + a.pad; }
+    else { ry[i] = yd * a.st - a.pad; rx[i] = xd * a.st - a.pad; }
+    akc[i] = swz(row, slot);
+  }
+  int bn_[LB], bkc[LB];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = a.bias[SCATTER ? (nb + r) % Cout : nb + r];
+  for (int i = 0; i < LB; ++i) {
+    const int row = wave * (BN / 4) + i * 16 + sub;
+    bn_[i] = n0 + row;
+    bkc[i] = swz(row, slot);
+  }
+  constexpr uint32_t BAD = 0xFFFFFFF0u;
+  const int KT = a.K / BK;
+  int tr = 0, ts = 0, tc = 0;                           // tap / channel cursor of the next K step to issue
+
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % STAGES) * STAGE;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      int ys, xs;
+      bool ok = rok[i];
+      if (TRANS) {
+        const int ty = ry[i] - tr, tx = rx[i] - ts;
+        if (a.st == 2) { ok = ok && !(ty & 1) && !(tx & 1); ys = ty >> 1; xs = tx >> 1; }
+        else { ys = ty; xs = tx; }
+        ok = ok && ty >= 0 && tx >= 0;
+      } else { ys = ry[i] + tr; xs = rx[i] + ts; ok = ok && ys >= 0 && xs >= 0; }
+      ok = ok && ys < a.Hs && xs < a.Ws;
+      const uint32_t off = ok ? (uint32_t)(((rbase[i] + ys * a.Ws + xs) * a.scs + tc + akc[i] * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_src, (__attribute__((address_space(3))) void*)(st + (wave * (BM / 4) + i * 16) * 64), 16, off, 0, 0, 0);
     }
+    const int k0 = kt * BK;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
+    for (int i = 0; i < LB; ++i) {
+      const bool ok = bn_[i] < a.Nout;
+      const uint32_t off = ok ? (uint32_t)((bn_[i] * a.K + k0 + bkc[i] * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_wgt, (__attribute__((address_space(3))) void*)(st + BM * 64 + (wave * (BN / 4) + i * 16) * 64), 16,
+          off, 0, 0, 0);
+    }
+    tc += BK;
+    if (tc == a.Cs) { tc = 0; if (++ts == a.S) { ts = 0; ++tr; } }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int D = STAGES - 1;                         // K steps in flight
+  constexpr int L = LA + LB;                            // DMA ops per wave per K step
+  for (int s = 0; s < D && s < KT; ++s) issue(s);
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    // retire stage kt (this wave's DMAs), then the barrier makes every wave's visible
+    if (kt + D <= KT) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((D - 1) * L) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the stage read at kt-1 is free for everyone now: refill it D steps ahead
+    if (kt + D < KT) issue(kt + D);
+    const char* sa = smem + (kt % STAGES) * STAGE;
+    const char* sb = sa + BM * 64;
+    bf16x8 xf[TM], wf[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-      if (!(m < m_end && nb < a.Nout)) continue;
-      if (EPI == 1) {
-        // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
-        const int ch = nb >> 2, Ch = a.Nout >> 2;
-        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-        const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
-        const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
-        const float c = gf * cp + gi * gg;
-        a.c_out[(size_t)m * Ch + ch] = c;
-        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanhf(c));
-        *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
-        continue;
-      }
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
-      size_t off;
-      if (SCATTER) {
-        const int blk = nb / Cout, co = nb - blk * Cout;
-        const int hw = a.Hd * a.Wd;
-        const int n = m / hw, rem = m - n * hw;
-        const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
-        const int yo = 2 * yd + (blk >> 1), xo = 2 * xd + (blk & 1);
-        off = ((size_t)(n * 2 * a.Hd + yo) * (2 * a.Wd) + xo) * a.dcs + co;
-      } else {
-        off = (size_t)m * a.dcs + nb;
-      }
-      if (a.accumulate) {
-        const uint2 old = *reinterpret_cast<const uint2*>(a.dst + off);
-        v[0] += __uint_as_float(old.x << 16);
-        v[1] += __uint_as_float(old.x & 0xffff0000u);
-        v[2] += __uint_as_float(old.y << 16);
-        v[3] += __uint_as_float(old.y & 0xffff0000u);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = round_bf(v[r]);
-      *reinterpret_cast<uint2*>(a.dst + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
+      const int row = wm * WTM + i * 16 + fr;
+      xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * 64 + swz(row, fk) * 16);
     }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * WTN + j * 16 + fr;
+      wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * 64 + swz(row, fk) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
   }
-  if (EPI != 0 || a.stats == nullptr) return;
-  // reduce over the 16 pixels held by lanes with equal fk, then over the WM waves
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        s1[j][r] += __shfl_xor(s1[j][r], o, 64);
-        s2[j][r] += __shfl_xor(s2[j][r], o, 64);
-      }
-  float* red = reinterpret_cast<float*>(smem);     // [WM][2][BN]
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if (fr == 0) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = wn * WTN + j * 16 + fk * 4 + r;
-        red[(wm * 2 + 0) * BN + col] = s1[j][r];
-        red[(wm * 2 + 1) * BN + col] = s2[j][r];
-      }
-  }
-  __syncthreads();
-  for (int col = tid; col < BN; col += NT) {
-    const int n = n0 + col;
-    if (n >= a.Nout) continue;
-    float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) { t1 += red[(w * 2) * BN + col]; t2 += red[(w * 2 + 1) * BN + col]; }
-    a.stats[(size_t)blockIdx.x * 2 * a.Nout + n] = t1;
-    a.stats[(size_t)blockIdx.x * 2 * a.Nout + a.Nout + n] = t2;
-  }
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, hipStream_t s) {
+int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, bool dma, uint32_t src_bytes,
+               hipStream_t s) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(NT);
+  if (dma && !smallc) {
+#define STF_D(TR, SCA, E) hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, TR, SCA, E, 4>), grid, block, 0, s, g, src_bytes)
+    if (lstm) STF_D(false, false, 1);
+    else if (scatter) STF_D(false, true, 0);
+    else if (trans) STF_D(true, false, 0);
+    else STF_D(false, false, 0);
+#undef STF_D
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
 #define STF_L(SC, TR, SCA, E) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA, E>), grid, block, 0, s, g)
   if (lstm) { if (smallc) return STF_EINVAL; STF_L(false, false, false, 1); }
   else if (scatter) { if (smallc) STF_L(true, false, true, 0); else STF_L(false, false, true, 0); }
@@ -269,6 +420,15 @@ int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, h
 #undef STF_L
   STF_CHECK_LAUNCH();
   return 0;
+}
+
+// STF_IGEMM_DMA=0 selects the register-staged kernel (A/B comparisons); read once.
+bool dma_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("STF_IGEMM_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 int pick_mtile(const stf_igemm_args* a) { return (a->Nout <= 64 && !a->lstm) ? 256 : 128; }
@@ -304,6 +464,11 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   }
   const bool smallc = (c.Cs % BK) != 0;
   hipStream_t s = (hipStream_t)stream;
-  if (bm == 256) return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
-  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
+  // LDS-DMA path needs byte offsets that fit the 32-bit buffer voffset
+  const uint64_t src_bytes = (uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2;
+  const uint64_t wgt_bytes = (uint64_t)g.Nout * g.K * 2;
+  const bool dma = dma_enabled() && src_bytes < 0xFFFFFF00ull && wgt_bytes < 0xFFFFFF00ull;
+  if (bm == 256)
+    return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, dma, (uint32_t)src_bytes, s);
+  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, dma, (uint32_t)src_bytes, s);
 }
