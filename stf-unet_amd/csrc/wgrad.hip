@@ -158,6 +158,153 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(WArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused-tap weight gradient for 3x3 / stride 1 / pad 1 convolutions.
+//
+// A block owns a 64 (dy channel) x 64 (x channel) tile for ALL nine taps and
+// walks a run of 2-D pixel tiles (PH x PW = 64 output pixels).  Per pixel tile
+// it stages the dy tile [64 px][64 n] and the x halo [(PH+2)(PW+2) px][64 c] in
+// LDS; the nine taps are nine shifted views of the halo, so every dy / x
+// element is read from HBM about once (the per-tap kernel above reads both 9x,
+// which bounds it by HBM at C = 64).  MFMA k-slot -> pixel is permuted so the
+// eight rows a 32-lane half reads with ds_read_b64_tr_b16 are eight consecutive
+// pixels, i.e. eight consecutive LDS rows (160 B stride: disjoint bank octets).
+// Waves: 2 (n) x 2 (c); each holds 32 n x 32 c x 9 taps = 36 accumulators.
+template <int PW>
+__global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles) {
+  constexpr int PH = 64 / PW, HW = PW + 2, HR = (PH + 2) * HW;
+  constexpr int SR = 64 + 16;                   // LDS row stride (elements), 160 B
+  constexpr int A_EL = 64 * SR, B_EL = HR * SR;
+  constexpr int CHA = 64 * 8 / NT;              // dy 16-B chunks per thread (2)
+  constexpr int CHB = (HR * 8 + NT - 1) / NT;   // halo chunks per thread
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2][A_EL + B_EL];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int split = blockIdx.x;
+  const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
+  const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
+  const int per_img = tiles_y * tiles_x;
+
+  uint4 ra[CHA], rb[CHB];
+  auto load = [&](int t) {
+    const int img = t / per_img, rem = t - img * per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * PH, x0 = tx * PW;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) {
+      const int e = tid + i * NT, px = e >> 3, ch = e & 7;
+      const int yd = y0 + px / PW, xd = x0 + px % PW;
+      ra[i] = make_uint4(0, 0, 0, 0);
+      if (yd < a.Hd && xd < a.Wd)
+        ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int e = tid + i * NT, hp = e >> 3, ch = e & 7;
+      const int ys = y0 - 1 + hp / HW, xs = x0 - 1 + hp % HW;
+      rb[i] = make_uint4(0, 0, 0, 0);
+      if (hp < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws)
+        rb[i] = *reinterpret_cast<const uint4*>(a.x + (size_t)((img * a.Hs + ys) * a.Ws + xs) * a.xcs + c0 + ch * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    uint16_t* sa = smem[buf];
+    uint16_t* sb = sa + A_EL;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) {
+      const int e = tid + i * NT;
+      *reinterpret_cast<uint4*>(sa + (e >> 3) * SR + (e & 7) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int e = tid + i * NT;
+      if (e < HR * 8) *reinterpret_cast<uint4*>(sb + (e >> 3) * SR + (e & 7) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // lane (g, q, p4): k-slot 8g + 4h + q (h = lo/hi read) holds pixel
+  // 16(g>>1) + 8h + 4(g&1) + q of the 32-pixel step.
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+  const int pl = 16 * (g >> 1) + 4 * (g & 1) + q;          // + 8h + kk
+  int arow[2][2], brow[2][2];                                // [kk/32][h]
+#pragma unroll
+  for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int px = 32 * k2 + 8 * h + pl;
+      arow[k2][h] = px * SR;
+      brow[k2][h] = ((px / PW) * HW + px % PW) * SR;
+    }
+
+  const int steps = t_end - t_begin;
+  if (steps > 0) { load(t_begin); store(0); }
+  __syncthreads();
+  for (int it = 0; it < steps; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < steps) load(t_begin + it + 1);
+    const uint16_t* sa = smem[cur];
+    const uint16_t* sb = sa + A_EL;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wm * 32 + i * 16 + p4;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][0] + col));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][1] + col));
+        short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, s8);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = ((t / 3) * HW + t % 3) * SR;
+        bf16x8 bfr[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = wn * 32 + j * 16 + p4;
+          v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][0] + toff + col));
+          v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][1] + toff + col));
+          short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[j] = __builtin_bit_cast(bf16x8, s8);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+      }
+    }
+    if (it + 1 < steps) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  const int RSC = 9 * a.Cs;
+  float* out = a.ws + (size_t)split * a.Nout * RSC;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = t * a.Cs + c0 + wn * 32 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+          out[(size_t)n * RSC + k] = acc[t][i][j][r];
+        }
+      }
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Nout, int R, int S,
                                     int Cs, float* __restrict__ out) {
   const int RSC = R * S * Cs;
@@ -174,7 +321,35 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, in
 
 bool big_tile(const stf_wgrad_args* a) { return a->Nout % 128 == 0 && a->g.Cs % 128 == 0; }
 
+// fused-tap kernel: 3x3, stride 1, pad 1, 64-multiples of channels, W >= 8
+int fused_pw(const stf_wgrad_args* a) {
+  static const bool enabled = [] { const char* e = getenv("STF_WGRAD_FUSED"); return !(e && e[0] == '0'); }();
+  const stf_conv_geom& c = a->g;
+  if (!enabled) return 0;
+  if (c.R != 3 || c.S != 3 || c.stride != 1 || c.pad != 1 || c.Hd != c.Hs || c.Wd != c.Ws) return 0;
+  if (a->Nout % 64 || c.Cs % 64 || c.Wd < 8) return 0;
+  return c.Wd >= 16 ? 16 : 8;
+}
+
+void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
+  ty = (a->g.Hd + 64 / pw - 1) / (64 / pw);
+  tx = (a->g.Wd + pw - 1) / pw;
+  nt = a->g.N * ty * tx;
+}
+
 void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
+  if (const int pw = fused_pw(a)) {
+    int ty, tx, nt;
+    fused_tiles(a, pw, ty, tx, nt);
+    const long tiles = (long)(a->Nout / 64) * (a->g.Cs / 64);
+    long want = (512 + tiles - 1) / tiles;
+    const long maxs = (nt + 3) / 4;                  // at least 4 pixel tiles per split
+    if (want > maxs) want = maxs;
+    if (want < 1) want = 1;
+    chunk = (int)((nt + want - 1) / want);
+    splits = (nt + chunk - 1) / chunk;
+    return;
+  }
   const int M = a->g.N * a->g.Hd * a->g.Wd;
   const int bm = big_tile(a) ? 128 : 64, bkp = big_tile(a) ? 32 : 64;
   const long rsc = (long)a->g.R * a->g.S * a->g.Cs;
@@ -211,7 +386,15 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.dycs = a->dy_cstride; w.chunk = chunk;
   hipStream_t s = (hipStream_t)stream;
   const int rsc = c.R * c.S * c.Cs;
-  if (big_tile(a)) {
+  if (const int pw = fused_pw(a)) {
+    int ty, tx, nt;
+    fused_tiles(a, pw, ty, tx, nt);
+    dim3 grid(splits, a->Nout / 64, c.Cs / 64);
+    if (pw == 16)
+      hipLaunchKernelGGL((wgrad3x3_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else
+      hipLaunchKernelGGL((wgrad3x3_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+  } else if (big_tile(a)) {
     dim3 grid(splits, a->Nout / 128, rsc / 128);
     hipLaunchKernelGGL((wgrad_kernel<128, 128, 32, false>), grid, dim3(NT), 0, s, w);
   } else if (c.Cs % 64 == 0) {

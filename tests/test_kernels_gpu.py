@@ -84,6 +84,26 @@ def test_wgrad(cin, cout, H, stride, R, pad):
     assert rel(out.view_as(w), w.grad) < 2e-3
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W,xcs,xoff,dycs", [
+    (3, 64, 64, 37, 21, 64, 0, 64),        # ragged 16x4 pixel tiles at both edges
+    (2, 128, 64, 32, 32, 192, 64, 64),     # x = slice of a concat buffer (dec1.0 shape)
+    (2, 64, 128, 12, 9, 64, 0, 192),       # W < 16 -> 8x8 pixel tiles; dy slice of wider rows
+    (1, 128, 128, 8, 8, 128, 0, 128),      # STF layer4-like 8x8
+    (16, 64, 64, 64, 64, 64, 0, 64),       # many pixel tiles per split
+])
+def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
+    """Fused-tap 3x3/s1/p1 weight gradient (one block = all nine taps)."""
+    from stfunet import nhwc
+    x = bfr(torch.randn(n, cin, H, W, device=DEV))
+    w = torch.randn(cout, cin, 3, 3, device=DEV).requires_grad_(True)
+    y = F.conv2d(x, w, padding=1)
+    dy = bfr(torch.randn_like(y))
+    y.backward(dy)
+    out = torch.empty(cout * cin * 9, device=DEV)
+    nhwc.wgrad(feat_from(dy, cs=dycs), feat_from(x, cs=xcs, off=xoff), 3, 3, 1, 1, out)
+    assert rel(out.view_as(w), w.grad) < 2e-3
+
+
 def test_conv_into_concat_slice():
     from stfunet import nhwc
     x = bfr(torch.randn(2, 64, 8, 8, device=DEV))
