@@ -37,9 +37,9 @@ STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // Shared epilogue: acc[i][j][r] = pixel m0 + wm*WTM + i*16 + (lane&15),
 // channel n0 + wn*WTN + j*16 + (lane>>4)*4 + r.
-template <int BM, int BN, int WM, int WN, bool SCATTER, int EPI>
+template <int BM, int BN, int WM, int WN, bool SCATTER, int EPI, int NTH>
 STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end, int n0,
-                            int wm, int wn, int tid, char* smem) {
+                            int wm, int wn, int tid, char* smem, int tile) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
@@ -123,14 +123,14 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
       }
   }
   __syncthreads();
-  for (int col = tid; col < BN; col += NT) {
+  for (int col = tid; col < BN; col += NTH) {
     const int n = n0 + col;
     if (n >= a.Nout) continue;
     float t1 = 0.f, t2 = 0.f;
 #pragma unroll
     for (int w = 0; w < WM; ++w) { t1 += red[(w * 2) * BN + col]; t2 += red[(w * 2 + 1) * BN + col]; }
-    a.stats[(size_t)blockIdx.x * 2 * a.Nout + n] = t1;
-    a.stats[(size_t)blockIdx.x * 2 * a.Nout + a.Nout + n] = t2;
+    a.stats[(size_t)tile * 2 * a.Nout + n] = t1;
+    a.stats[(size_t)tile * 2 * a.Nout + a.Nout + n] = t2;
   }
 }
 
@@ -266,45 +266,65 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
     __syncthreads();
   }
 
-  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NT>(a, acc, m0, m_end, n0, wm, wn, tid, smem, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
-// LDS-DMA ring variant (Cs % 32 == 0): every 16-B chunk goes global -> LDS with
+// LDS-DMA ring variant (Cs % BKK == 0): every 16-B chunk goes global -> LDS with
 // buffer_load_dwordx4 ... lds (no VGPR staging, no ds_write).  The im2col halo
 // and all tails are zero-filled by the buffer range check: an invalid lane gets
-// voffset 0xFFFFFFF0 >= num_records.  One wave-instruction writes 1 KiB = 16
-// rows x 64 B linearly, so the chunk swizzle is applied on the SOURCE side (lane
-// with LDS chunk slot p loads global chunk p ^ swz(row)); the fragment reads use
-// the same involution.  STAGES-deep ring, STAGES-1 K steps in flight across the
-// raw s_barrier; a counted vmcnt retires exactly the stage about to be read.
-template <int BM, int BN, int WM, int WN, bool TRANS, bool SCATTER, int EPI, int STAGES>
-__global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(Geo a, uint32_t src_bytes) {
+// voffset 0xFFFFFFF0 >= num_records.  One wave-instruction writes 1 KiB of rows
+// linearly, so the chunk swizzle is applied on the SOURCE side (lane with LDS
+// chunk slot p loads global chunk swz(row, p)); the fragment reads use the same
+// involution.  STAGES-deep ring, STAGES-1 K steps in flight across the raw
+// s_barrier; a counted vmcnt retires exactly the stage about to be read.
+//   BKK = 32: 64-B rows, chunk ^ ((-(row>>2)) & 3)
+//   BKK = 64: 128-B rows, chunk ^ ((row>>1) & 7)   (two MFMA k-halves per step)
+// Both make each ds_read_b128 lane group (4 x 16 lanes) hit 16 distinct 16-B
+// slots of the 256-B bank row.  Blocks are remapped so that consecutive tiles
+// (shared halo rows) and all channel tiles of one pixel tile run on one XCD.
+template <int BKK>
+STF_DEV int swzk(int row, int kc) {
+  if constexpr (BKK == 32) return kc ^ ((-(row >> 2)) & 3);
+  else return kc ^ ((row >> 1) & 7);
+}
+
+template <int BM, int BN, int WM, int WN, int BKK, int STAGES, bool TRANS, bool SCATTER, int EPI>
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dma_kernel(Geo a, uint32_t src_bytes) {
+  constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int LA = BM / 64, LB = BN / 64;            // DMA instructions per wave per K step
-  constexpr int STAGE = (BM + BN) * 64;                 // bytes per ring stage
+  constexpr int ROWB = BKK * 2;                         // bytes per LDS row
+  constexpr int CPR = BKK / 8;                          // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;                         // rows per DMA wave-instruction (1 KiB)
+  constexpr int LA = BM / NW / RPI, LB = BN / NW / RPI; // DMA instructions per wave per K step
+  constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int LDS_MAIN = STAGES * STAGE, LDS_RED = WM * 2 * BN * 4;
-  static_assert(WM * WN == 4 && LA >= 1 && LB >= 1, "tile");
+  static_assert(LA >= 1 && LB >= 1 && LA * RPI * NW == BM && LB * RPI * NW == BN, "tile");
   __shared__ __attribute__((aligned(16))) char smem[LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int grp = blockIdx.x / a.tpg, gtile = blockIdx.x - grp * a.tpg;
-  const int m0 = grp * a.Mg + gtile * BM, n0 = blockIdx.y * BN;
+  // XCD-aware bijective remap of the linear block id (8 XCDs, round-robin dispatch)
+  const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy;
+  const int orig = blockIdx.y * gx + blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int bx = wid / gy, by = wid - bx * gy;
+  const int grp = bx / a.tpg, gtile = bx - grp * a.tpg;
+  const int m0 = grp * a.Mg + gtile * BM, n0 = by * BN;
   const int m_end = min(m0 + BM, min((grp + 1) * a.Mg, a.M));
-  const int sub = lane >> 2, slot = lane & 3;
+  const int sub = lane / CPR, slot = lane % CPR;
 
   const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_wgt =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, 0, (uint32_t)a.Nout * a.K * 2, 0x00020000);
 
-  // per-lane gather state: one im2col row per A instruction, one weight row per B instruction
   int rbase[LA], ry[LA], rx[LA], akc[LA];
   bool rok[LA];
 #pragma unroll
   for (int i = 0; i < LA; ++i) {
-    const int row = wave * (BM / 4) + i * 16 + sub;
+    const int row = wave * (BM / NW) + i * RPI + sub;
     const int m = m0 + row;
     rok[i] = m < m_end;
     const int mm = rok[i] ? m : m0;
@@ -314,17 +334,17 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(Geo a, uint32_t src_by
     rbase[i] = n * a.Hs * a.Ws;
     if (TRANS) { ry[i] = yd + a.pad; rx[i] = xd + a.pad; }
     else { ry[i] = yd * a.st - a.pad; rx[i] = xd * a.st - a.pad; }
-    akc[i] = swz(row, slot);
+    akc[i] = swzk<BKK>(row, slot);
   }
   int bn_[LB], bkc[LB];
 #pragma unroll
   for (int i = 0; i < LB; ++i) {
-    const int row = wave * (BN / 4) + i * 16 + sub;
+    const int row = wave * (BN / NW) + i * RPI + sub;
     bn_[i] = n0 + row;
-    bkc[i] = swz(row, slot);
+    bkc[i] = swzk<BKK>(row, slot);
   }
   constexpr uint32_t BAD = 0xFFFFFFF0u;
-  const int KT = a.K / BK;
+  const int KT = a.K / BKK;
   int tr = 0, ts = 0, tc = 0;                           // tap / channel cursor of the next K step to issue
 
   auto issue = [&](int kt) {
@@ -342,18 +362,19 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(Geo a, uint32_t src_by
       ok = ok && ys < a.Hs && xs < a.Ws;
       const uint32_t off = ok ? (uint32_t)(((rbase[i] + ys * a.Ws + xs) * a.scs + tc + akc[i] * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_src, (__attribute__((address_space(3))) void*)(st + (wave * (BM / 4) + i * 16) * 64), 16, off, 0, 0, 0);
+          rs_src, (__attribute__((address_space(3))) void*)(st + (wave * (BM / NW) + i * RPI) * ROWB), 16, off, 0, 0,
+          0);
     }
-    const int k0 = kt * BK;
+    const int k0 = kt * BKK;
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const bool ok = bn_[i] < a.Nout;
       const uint32_t off = ok ? (uint32_t)((bn_[i] * a.K + k0 + bkc[i] * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_wgt, (__attribute__((address_space(3))) void*)(st + BM * 64 + (wave * (BN / 4) + i * 16) * 64), 16,
-          off, 0, 0, 0);
+          rs_wgt, (__attribute__((address_space(3))) void*)(st + BM * ROWB + (wave * (BN / NW) + i * RPI) * ROWB),
+          16, off, 0, 0, 0);
     }
-    tc += BK;
+    tc += BKK;
     if (tc == a.Cs) { tc = 0; if (++ts == a.S) { ts = 0; ++tr; } }
   };
 
@@ -375,51 +396,47 @@ __global__ __launch_bounds__(NT, 2) void igemm_dma_kernel(Geo a, uint32_t src_by
     // the stage read at kt-1 is free for everyone now: refill it D steps ahead
     if (kt + D < KT) issue(kt + D);
     const char* sa = smem + (kt % STAGES) * STAGE;
-    const char* sb = sa + BM * 64;
-    bf16x8 xf[TM], wf[TN];
+    const char* sb = sa + BM * ROWB;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * WTM + i * 16 + fr;
-      xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * 64 + swz(row, fk) * 16);
+    for (int h = 0; h < BKK / 32; ++h) {
+      bf16x8 xf[TM], wf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + fr;
+        xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 16 + fr;
+        wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wn * WTN + j * 16 + fr;
-      wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * 64 + swz(row, fk) * 16);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx);
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_cfg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, bool dma, uint32_t src_bytes,
-               hipStream_t s) {
-  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(NT);
-  if (dma && !smallc) {
-#define STF_D(TR, SCA, E) hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, TR, SCA, E, 4>), grid, block, 0, s, g, src_bytes)
-    if (lstm) STF_D(false, false, 1);
-    else if (scatter) STF_D(false, true, 0);
-    else if (trans) STF_D(true, false, 0);
-    else STF_D(false, false, 0);
-#undef STF_D
-    STF_CHECK_LAUNCH();
-    return 0;
-  }
-#define STF_L(SC, TR, SCA, E) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA, E>), grid, block, 0, s, g)
-  if (lstm) { if (smallc) return STF_EINVAL; STF_L(false, false, false, 1); }
-  else if (scatter) { if (smallc) STF_L(true, false, true, 0); else STF_L(false, false, true, 0); }
-  else if (trans) { if (smallc) STF_L(true, true, false, 0); else STF_L(false, true, false, 0); }
-  else { if (smallc) STF_L(true, false, false, 0); else STF_L(false, false, false, 0); }
-#undef STF_L
-  STF_CHECK_LAUNCH();
-  return 0;
+// Tile configurations of the DMA kernel.  'auto' picks per shape; the
+// STF_IGEMM_CFG environment variable forces one (A/B measurements).
+struct Cfg { int bm, bn, bkk; };
+constexpr Cfg CFG_A{128, 128, 32};   // 4 waves (2x2), 4 stages, 2 blocks/CU
+constexpr Cfg CFG_B{256, 128, 64};   // 8 waves (4x2), 3 stages
+constexpr Cfg CFG_C{256, 256, 64};   // 8 waves (2x4), 2 stages
+constexpr Cfg CFG_D{512, 64, 64};    // 8 waves (8x1), 2 stages
+constexpr Cfg CFG_E{256, 64, 32};    // 4 waves (4x1), 4 stages, 2 blocks/CU
+
+char forced_cfg() {
+  static const char c = [] {
+    const char* e = getenv("STF_IGEMM_CFG");
+    return (e && e[0] >= 'A' && e[0] <= 'E') ? e[0] : '0';
+  }();
+  return c;
 }
 
 // STF_IGEMM_DMA=0 selects the register-staged kernel (A/B comparisons); read once.
@@ -431,7 +448,84 @@ bool dma_enabled() {
   return on;
 }
 
-int pick_mtile(const stf_igemm_args* a) { return (a->Nout <= 64 && !a->lstm) ? 256 : 128; }
+// which kernel runs: 'R' = register-staged (BM 256 for Nout <= 64, else 128), or a DMA config letter
+char choose(const stf_igemm_args* a, bool dma_ok) {
+  const stf_conv_geom& c = a->g;
+  const bool plain = !a->lstm && !a->scatter2x2 && !c.transposed;
+  if (!dma_enabled() || !dma_ok || c.Cs % 32) return 'R';
+  const char f = forced_cfg();
+  const bool bk64 = c.Cs % 64 == 0;
+  if (f != '0') {
+    if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
+    if (plain && bk64) return f;
+  }
+  if (plain && bk64) {
+    // measured per layer (tools/bench_layers.py, cfg2 shapes): C where it fills the chip,
+    // B for 128-multiples, D for 64 output channels
+    const long M = (long)c.N * c.Hd * c.Wd;
+    const long blocks_c = ((M + 255) / 256) * ((a->Nout + 255) / 256);
+    if (a->Nout % 256 == 0 && blocks_c >= 240) return 'C';
+    if (a->Nout % 128 == 0) return 'B';
+    if (a->Nout == 64) return 'D';
+  }
+  if (a->Nout <= 64 && !a->lstm) return 'E';
+  return 'A';
+}
+
+Cfg cfg_of(char k) {
+  switch (k) {
+    case 'B': return CFG_B;
+    case 'C': return CFG_C;
+    case 'D': return CFG_D;
+    case 'E': return CFG_E;
+    default: return CFG_A;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
+void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, uint32_t src_bytes, hipStream_t s) {
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
+#define STF_D(TR, SCA, E) \
+  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, TR, SCA, E>), grid, block, 0, s, g, src_bytes)
+  if (lstm) STF_D(false, false, 1);
+  else if (scatter) STF_D(false, true, 0);
+  else if (trans) STF_D(true, false, 0);
+  else STF_D(false, false, 0);
+#undef STF_D
+}
+
+template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
+void launch_dma_plain(const Geo& g, uint32_t src_bytes, hipStream_t s) {
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
+  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 0>), grid, block, 0, s, g,
+                     src_bytes);
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_reg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, hipStream_t s) {
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(NT);
+#define STF_L(SC, TR, SCA, E) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA, E>), grid, block, 0, s, g)
+  if (lstm) { if (smallc) return STF_EINVAL; STF_L(false, false, false, 1); }
+  else if (scatter) { if (smallc) STF_L(true, false, true, 0); else STF_L(false, false, true, 0); }
+  else if (trans) { if (smallc) STF_L(true, true, false, 0); else STF_L(false, true, false, 0); }
+  else { if (smallc) STF_L(true, false, false, 0); else STF_L(false, false, false, 0); }
+#undef STF_L
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+bool dma_fits(const stf_igemm_args* a) {
+  const stf_conv_geom& c = a->g;
+  const uint64_t src_bytes = (uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2;
+  const uint64_t wgt_bytes = (uint64_t)a->Nout * c.R * c.S * c.Cs * 2;
+  return src_bytes < 0xFFFFFF00ull && wgt_bytes < 0xFFFFFF00ull;
+}
+
+int pick_mtile(const stf_igemm_args* a) {
+  const char k = choose(a, dma_fits(a));
+  if (k == 'R') return (a->Nout <= 64 && !a->lstm) ? 256 : 128;
+  return cfg_of(k).bm;
+}
 
 }  // namespace
 
@@ -464,11 +558,17 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   }
   const bool smallc = (c.Cs % BK) != 0;
   hipStream_t s = (hipStream_t)stream;
-  // LDS-DMA path needs byte offsets that fit the 32-bit buffer voffset
-  const uint64_t src_bytes = (uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2;
-  const uint64_t wgt_bytes = (uint64_t)g.Nout * g.K * 2;
-  const bool dma = dma_enabled() && src_bytes < 0xFFFFFF00ull && wgt_bytes < 0xFFFFFF00ull;
-  if (bm == 256)
-    return launch_cfg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, dma, (uint32_t)src_bytes, s);
-  return launch_cfg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, dma, (uint32_t)src_bytes, s);
+  const uint32_t src_bytes = (uint32_t)((uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2);
+  switch (choose(a, dma_fits(a))) {
+    case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
+    case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
+    case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, src_bytes, s); break;
+    case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, src_bytes, s); break;
+    case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, src_bytes, s); break;
+    default:
+      if (bm == 256) return launch_reg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
+      return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
+  }
+  STF_CHECK_LAUNCH();
+  return 0;
 }
