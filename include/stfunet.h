@@ -68,20 +68,22 @@ typedef struct stf_igemm_args {
   void* dst;           /* bf16, first channel of the destination slice          */
   int dst_cstride;
   const float* bias;   /* [Nout] (scatter2x2: [Nout/4]) or NULL                 */
-  float* stats;        /* [mtiles][2][Nout] per-tile (sum, sum of squares) of   */
-                       /* the stored bf16 outputs, or NULL                      */
+  float* stats;        /* [tiles][2][Nout] per-tile (sum, sum of squares) of    */
+                       /* the stored bf16 outputs, or NULL (tiles: see          */
+                       /* stf_igemm_stat_tiles)                                 */
   int scatter2x2;      /* 1: ConvTranspose2d(k=2,s=2) epilogue: column          */
                        /* n = (dy*2+dx)*Cout + co lands on pixel (2yd+dy,2xd+dx)*/
                        /* of a [N][2Hd][2Wd] destination                        */
-  int group_rows;      /* >0: M tiles aligned to groups of this many rows and   */
-                       /* stats laid out [M/group_rows][mtiles/group][2][Nout]  */
+  int group_rows;      /* >0: tiles aligned to groups of this many rows (whole  */
+                       /* images) and stats laid out [M/group_rows][tiles][2][Nout] */
                        /* (per-time-step BatchNorm of the batched STF encoder)  */
   int accumulate;      /* 1: dst += result (bf16 read-modify-write)             */
   const stf_lstm_epi* lstm; /* non-NULL: LSTM cell epilogue, dst unused          */
 } stf_igemm_args;
 
-/* Rows per M tile chosen for these args (size `stats` as groups*ceil(rows_per_group/mtile)). */
-int stf_igemm_mtile(const stf_igemm_args* a);
+/* Partial-statistics rows per group for these args (the tiling depends on the
+ * kernel chosen): size `stats` as groups * stf_igemm_stat_tiles(a) * 2 * Nout. */
+int stf_igemm_stat_tiles(const stf_igemm_args* a);
 /* Conv2d 3x3/1x1/strided forward with fused bias + BatchNorm partial statistics
  *   replaces nn.Conv2d in conv_block  (src/unet.py:12,15), ResidualConvBlock
  *   (src/stf_lstm_unet.py:13,16,23), ResNet-34 convs (src/stf_lstm_unet.py:108-114),

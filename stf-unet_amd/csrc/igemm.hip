@@ -35,11 +35,12 @@ STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
 
 STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-// Shared epilogue: acc[i][j][r] = pixel m0 + wm*WTM + i*16 + (lane&15),
-// channel n0 + wn*WTN + j*16 + (lane>>4)*4 + r.
+// Shared epilogue: acc[i][j][r] = pixel mrow[i] (this lane's GEMM row of
+// fragment i, -1 = outside the image / tile), channel n0 + wn*WTN + j*16 +
+// (lane>>4)*4 + r.  `tile` indexes the BatchNorm partial-statistics row.
 template <int BM, int BN, int WM, int WN, bool SCATTER, int EPI, int NTH>
-STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end, int n0,
-                            int wm, int wn, int tid, char* smem, int tile) {
+STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], const int (&mrow)[BM / WM / 16],
+                            int n0, int wm, int wn, int tid, char* smem, int tile) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
@@ -57,8 +58,8 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
     for (int r = 0; r < 4; ++r) { s1[j][r] = 0.f; s2[j][r] = 0.f; }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-      if (!(m < m_end && nb < a.Nout)) continue;
+      const int m = mrow[i];
+      if (!(m >= 0 && nb < a.Nout)) continue;
       if (EPI == 1) {
         // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
         const int ch = nb >> 2, Ch = a.Nout >> 2;
@@ -266,7 +267,13 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
     __syncthreads();
   }
 
-  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NT>(a, acc, m0, m_end, n0, wm, wn, tid, smem, blockIdx.x);
+  int mrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + (lane & 15);
+    mrow[i] = m < m_end ? m : -1;
+  }
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NT>(a, acc, mrow, n0, wm, wn, tid, smem, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -419,7 +426,253 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx);
+  int mrow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + fr;
+    mrow[i] = m < m_end ? m : -1;
+  }
+  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NTH>(a, acc, mrow, n0, wm, wn, tid, smem, bx);
+}
+
+
+// ---------------------------------------------------------------------------
+// Halo kernel: 3x3 / stride 1 / pad 1 convolution (forward, and the stride-1
+// dgrad over flipped taps) as nine shifted views of one LDS halo.
+//
+// The linear kernels above gather the source rows of every tap separately, so
+// each activation row crosses L2 -> LDS nine times; for the 64-channel
+// full-resolution layers that re-read traffic (~26 GB/s per CU) is the bound.
+// Here a workgroup owns a PH x PW pixel tile and a 64-channel output slice; per
+// 32-channel source chunk one stage holds the (PH+2) x (PW+2) halo and the 64 x
+// 9 weight rows of that chunk, and the nine taps are read from the halo at row
+// offsets (r * (PW+2) + s).  Persistent: each workgroup walks a contiguous run
+// of (tile, channel-slice) items through a 2-stage LDS-DMA ring, so the next
+// stage streams in behind the MFMAs and the epilogue.  Rows are 64 B with the
+// chunk swizzle kc ^ ((row >> 1) & 2), conflict-free for ds_read_b128 at ANY
+// row offset (a tap shift moves the 16 rows a fragment reads by 0..2 rows).
+STF_DEV int swzh(int row, int kc) { return kc ^ ((row >> 1) & 2); }
+
+template <int PH, int PW, int DIAG>
+__global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
+                                                            int rem) {
+  constexpr int NW = 8, BN = 64, RPI = 16;              // 64-B rows: 16 per 1-KiB DMA instruction
+  constexpr int HW = PW + 2, HR = (PH + 2) * HW;        // halo rows
+  constexpr int HI = (HR + RPI * NW - 1) / (RPI * NW);  // halo DMA instructions per wave
+  constexpr int WI = (9 * BN + RPI * NW - 1) / (RPI * NW);
+  constexpr int HROWS = HI * RPI * NW, WROWS = WI * RPI * NW;
+  constexpr int STAGE = (HROWS + WROWS) * 64;
+  constexpr int PX = PH * PW, WTM = PX / NW, TM = WTM / 16, TN = BN / 16;
+  static_assert(PX % (16 * NW) == 0 && PW % 16 == 0 && PX == 512, "tile (epilogue: 8 stores per lane)");
+  static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE, "epilogue scratch");
+  static_assert(2 * STAGE <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
+  const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
+  const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
+  const int it0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  const int S = cnt * CC;
+  if (S == 0) return;
+
+  const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_wgt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, 0, (uint32_t)a.Nout * a.K * 2, 0x00020000);
+  constexpr uint32_t BAD = 0xFFFFFFF0u;
+  // NULL bias -> zero-sized range: the loads return 0 without a branch
+  const __amdgpu_buffer_rsrc_t rs_bias = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bias, 0, a.bias ? (uint32_t)a.Nout * 4 : 0u, 0x00020000);
+
+  // live = false: a dummy stage (all lanes out of range) so every iteration issues the same DMA count
+  auto issue = [&](int item, int cc, int buf, bool live) {
+    const int nt = item % NTn, tile = item / NTn;
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    const int y0 = ty * PH - 1, x0 = tx * PW - 1;
+    char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int hr = (wave * HI + i) * RPI + sub;
+      const int hy = hr / HW, hx = hr - hy * HW;
+      const int ys = y0 + hy, xs = x0 + hx;
+      const bool ok = live && hr < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws;
+      const uint32_t off =
+          ok ? (uint32_t)((((img * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hr, slot) * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_src, (__attribute__((address_space(3))) void*)(st + (wave * HI + i) * RPI * 64), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
+      const int tap = wr >> 6, n = nt * BN + (wr & 63);
+      const bool ok = live && wr < 9 * BN;
+      const uint32_t off = ok ? (uint32_t)(((size_t)n * a.K + tap * a.Cs + cc * 32 + swzh(wr, slot) * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs_wgt, (__attribute__((address_space(3))) void*)(st + (HROWS + (wave * WI + i) * RPI) * 64), 16, off, 0,
+          0, 0);
+    }
+  };
+
+  int hbase[TM];                                        // halo row of this lane's pixel, tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = wave * WTM + i * 16 + fr;
+    hbase[i] = (p / PW) * HW + p % PW;
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue(it0, 0, 0, true);
+  int iit = it0, icc = 0;                               // issue cursor (last issued stage)
+  int cit = it0, ccc = 0;                               // compute cursor
+  bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
+  for (int s = 0; s < S; ++s) {
+    // retire this stage's DMA; the previous epilogue's 8 buffer stores (issued
+    // after it, stores and loads retire in order) may stay in flight
+    if (epi) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    epi = false;
+    __builtin_amdgcn_s_barrier();
+    // bias of this lane's 16 accumulator channels, loaded BEFORE the next DMA so
+    // that waiting for it never waits for the DMA
+    f32x4 bv[TN];
+    if (ccc == CC - 1) {
+      const int nt = cit % NTn;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bv[j] = __builtin_amdgcn_raw_buffer_load_b128(rs_bias, (nt * BN + j * 16 + fk * 4) * 4, 0, 0);
+    }
+    {
+      const bool live = s + 1 < S;
+      if (live && ++icc == CC) { icc = 0; ++iit; }
+      issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
+    }
+    const char* hb = smem + (s & 1) * STAGE;
+    if (DIAG == 3) { if (++ccc == CC) { ccc = 0; ++cit; } continue; }
+    const char* wb = hb + HROWS * 64;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * HW + (t % 3);
+      bf16x8 xf[TM], wf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = hbase[i] + toff;
+        xf[i] = *reinterpret_cast<const bf16x8*>(hb + row * 64 + swzh(row, fk) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = t * BN + j * 16 + fr;
+        wf[j] = *reinterpret_cast<const bf16x8*>(wb + row * 64 + swzh(row, fk) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+    }
+    if (++ccc == CC) {
+      // ---- epilogue through LDS: the stage just read becomes the output tile
+      // [PX][64] bf16 (128-B rows, 16-B chunk c at c ^ (p & 7)); full-row 16-B
+      // buffer stores (invalid pixels get an out-of-range offset, so every lane
+      // issues exactly 8 stores and the next stage can wait with vmcnt(8));
+      // BN partial sums from the stored values; raw barriers only, so nothing
+      // drains the stores or the DMA already in flight.
+      const int nt = cit % NTn, tile = cit / NTn;
+      const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+      char* ot = smem + (s & 1) * STAGE;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                     // every wave is done reading this stage
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int p = wave * WTM + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int ch = j * 16 + fk * 4, c16 = ch >> 3;
+          const uint2 v = make_uint2(pack2(acc[i][j][0] + bv[j][0], acc[i][j][1] + bv[j][1]),
+                                     pack2(acc[i][j][2] + bv[j][2], acc[i][j][3] + bv[j][3]));
+          *reinterpret_cast<uint2*>(ot + p * 128 + ((c16 ^ (p & 7)) << 4) + (ch & 7) * 2) = v;
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const int c16 = tid & 7;
+      const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
+      const __amdgpu_buffer_rsrc_t rs_dst = __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
+      float s1[8], s2[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+      for (int k = 0; k < PX / 64; ++k) {
+        const int p = (tid >> 3) + 64 * k;
+        const int y = ty * PH + p / PW, x = tx * PW + p % PW;
+        const bool ok = y < a.Hd && x < a.Wd;
+        const int m = (img * a.Hd + y) * a.Wd + x;
+        uint4 u = *reinterpret_cast<const uint4*>(ot + p * 128 + ((c16 ^ (p & 7)) << 4));
+        const uint32_t off = ok ? (uint32_t)(((size_t)m * a.dcs + nt * BN + c16 * 8) * 2) : 0xFFFFFFF0u;
+        float f[8];
+        unpack8(u, f);
+        if (a.accumulate && ok) {
+          float o[8];
+          unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)m * a.dcs + nt * BN + c16 * 8), o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = round_bf(f[e] + o[e]);
+          u = pack8(f);
+        }
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        if (ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
+        }
+      }
+      if (a.stats) {
+        // lanes with equal (lane & 7) hold the same 8 channels: fold 8 -> 1 per wave, then over waves
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int o = 8; o < 64; o <<= 1) {
+            s1[e] += __shfl_xor(s1[e], o, 64);
+            s2[e] += __shfl_xor(s2[e], o, 64);
+          }
+        float* red = reinterpret_cast<float*>(ot + PX * 128);   // [NW][2][64]
+        if (lane < 8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[(wave * 2 + 0) * 64 + lane * 8 + e] = s1[e];
+            red[(wave * 2 + 1) * 64 + lane * 8 + e] = s2[e];
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (tid < 128) {
+          const int q = tid >> 6, col = tid & 63;
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
+          a.stats[(size_t)tile * 2 * a.Nout + q * a.Nout + nt * BN + col] = t;
+        }
+      }
+      ccc = 0;
+      ++cit;
+      epi = true;
+    }
+  }
+}
+
+constexpr int HALO_PH = 16, HALO_PW = 32;
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
 }
 
 // Tile configurations of the DMA kernel.  'auto' picks per shape; the
@@ -434,7 +687,7 @@ constexpr Cfg CFG_E{256, 64, 32};    // 4 waves (4x1), 4 stages, 2 blocks/CU
 char forced_cfg() {
   static const char c = [] {
     const char* e = getenv("STF_IGEMM_CFG");
-    return (e && e[0] >= 'A' && e[0] <= 'E') ? e[0] : '0';
+    return (e && ((e[0] >= 'A' && e[0] <= 'E') || e[0] == 'H' || e[0] == 'L')) ? e[0] : '0';
   }();
   return c;
 }
@@ -455,7 +708,12 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   if (!dma_enabled() || !dma_ok || c.Cs % 32) return 'R';
   const char f = forced_cfg();
   const bool bk64 = c.Cs % 64 == 0;
-  if (f != '0') {
+  const bool halo_ok = plain && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs &&
+                       c.Wd == c.Ws && a->Nout % 64 == 0;
+  if (f == 'H' && halo_ok) return 'H';
+  // auto: the halo kernel for full-size 3x3 layers ('L' = auto over the linear kernels only)
+  if (f == '0' && halo_ok && c.Wd >= 32) return 'H';
+  if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
     if (plain && bk64) return f;
   }
@@ -527,9 +785,28 @@ int pick_mtile(const stf_igemm_args* a) {
   return cfg_of(k).bm;
 }
 
+void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
+  ty = (c.Hd + HALO_PH - 1) / HALO_PH;
+  tx = (c.Wd + HALO_PW - 1) / HALO_PW;
+}
+
+// BatchNorm partial-statistics rows per group for the kernel that will run
+int stat_tiles(const stf_igemm_args* a) {
+  const stf_conv_geom& c = a->g;
+  const long M = (long)c.N * c.Hd * c.Wd;
+  const long Mg = a->group_rows > 0 ? a->group_rows : M;
+  if (choose(a, dma_fits(a)) == 'H') {
+    int ty, tx;
+    halo_tiles(c, ty, tx);
+    return (int)(Mg / ((long)c.Hd * c.Wd)) * ty * tx;
+  }
+  const int bm = pick_mtile(a);
+  return (int)((Mg + bm - 1) / bm);
+}
+
 }  // namespace
 
-extern "C" int stf_igemm_mtile(const stf_igemm_args* a) { return pick_mtile(a); }
+extern "C" int stf_igemm_stat_tiles(const stf_igemm_args* a) { return stat_tiles(a); }
 
 extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   const stf_conv_geom& c = a->g;
@@ -559,7 +836,22 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   const bool smallc = (c.Cs % BK) != 0;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t src_bytes = (uint32_t)((uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2);
-  switch (choose(a, dma_fits(a))) {
+  const char k = choose(a, dma_fits(a));
+  if (k == 'H') {
+    if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
+    int ty, tx;
+    halo_tiles(c, ty, tx);
+    const long items = (long)c.N * ty * tx * (a->Nout / 64);
+    const int grid = (int)std::min<long>(items, num_cus());
+    static const int diag = [] { const char* e = getenv("STF_HALO_DIAG"); return e ? atoi(e) : 0; }();
+#define STF_H(D) hipLaunchKernelGGL((conv3x3_halo_kernel<HALO_PH, HALO_PW, D>), dim3(grid), dim3(512), 0, s, g, \
+                                    src_bytes, ty, tx, (int)(items / grid), (int)(items % grid))
+    if (diag == 1) STF_H(1); else if (diag == 2) STF_H(2); else if (diag == 3) STF_H(3); else STF_H(0);
+#undef STF_H
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
+  switch (k) {
     case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
     case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
     case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, src_bytes, s); break;

@@ -143,8 +143,7 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
                   ctypes.pointer(lstm) if lstm is not None else None)
     stats, tiles = None, 0
     if want_stats:
-        mt = _lib.load().stf_igemm_mtile(ctypes.byref(a))
-        tiles = (M // groups + mt - 1) // mt
+        tiles = _lib.load().stf_igemm_stat_tiles(ctypes.byref(a))
         stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
         a.stats = _p(stats)
     t = TIMER

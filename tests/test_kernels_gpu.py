@@ -104,6 +104,43 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     assert rel(out.view_as(w), w.grad) < 2e-3
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W,groups,acc,xcs,xoff", [
+    (2, 64, 64, 37, 70, 1, False, 64, 0),        # ragged 16x32 halo tiles at both edges
+    (4, 128, 128, 64, 64, 2, False, 192, 64),    # grouped statistics, source = concat slice
+    (2, 32, 128, 20, 96, 1, True, 32, 0),        # one 32-channel chunk, accumulate into dst
+    (1, 96, 64, 64, 80, 1, False, 96, 0),        # three chunks
+])
+def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
+    """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
+    BN partial statistics, accumulate, and the stride-1 dgrad over flipped taps."""
+    from stfunet import nhwc
+    x = bfr(torch.randn(n, cin, H, W, device=DEV))
+    w = bfr(torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5)
+    b = torch.randn(cout, device=DEV)
+    ref = F.conv2d(x, w, b, padding=1)
+    dst = nhwc.new_feat(n, H, W, cout, DEV)
+    base = None
+    if acc:
+        base = bfr(torch.randn_like(ref))
+        dst.buf.view(n, H, W, cout).copy_(base.permute(0, 2, 3, 1).to(torch.bfloat16))
+        ref = ref + base
+    stats, tiles = nhwc.igemm(feat_from(x, cs=xcs, off=xoff), nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst,
+                              3, 3, 1, 1, bias=b, want_stats=True, groups=groups, accumulate=acc)
+    out = dst.dense()
+    assert rel(out, ref) < 1e-2
+    st = stats.view(groups, tiles, 2, cout).sum(1)
+    og = out.view(groups, n // groups, cout, H, W)
+    for g in range(groups):
+        assert rel(st[g, 0], og[g].sum((0, 2, 3))) < 2e-3
+        assert rel(st[g, 1], (og[g] ** 2).sum((0, 2, 3))) < 2e-3
+    dy = bfr(torch.randn(n, cout, H, W, device=DEV))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(dy)
+    dx = nhwc.new_feat(n, H, W, cin, DEV)
+    nhwc.conv_dgrad(feat_from(dy), w.contiguous(), dx, 3, 3, 1, 1)
+    assert rel(dx.dense(), xr.grad) < 1e-2
+
+
 def test_conv_into_concat_slice():
     from stfunet import nhwc
     x = bfr(torch.randn(2, 64, 8, 8, device=DEV))
