@@ -35,35 +35,38 @@ STF_DEV void load_affine(const float* p, int c, float (&v)[8]) {
 
 int tiles_per_group(long units_per_group, int groups) {
   long t = (units_per_group + NT - 1) / NT;
-  const long cap = (1024 + groups - 1) / groups;
+  const long cap = (1024 + groups - 1) / groups;    // <= FOLD16_ROWS partial rows per group
   if (t > cap) t = cap;
   if (t < 1) t = 1;
   return (int)t;
 }
 
 // ------------------------------------------------------------------ finalize
-// stats: [G][T][2][C] with the first S rows of every group folded.  One thread
-// per channel walks the groups in order so running stats see G sequential updates.
-__global__ void bn_finalize_kernel(const float* __restrict__ stats, int S, int T, int G, int C, long Mg,
-                                   const float* gamma, const float* beta, float mom, float eps,
-                                   float* rm, float* rv, float* mean, float* invstd, float* scale,
-                                   float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float run_m = rm ? rm[c] : 0.f, run_v = rv ? rv[c] : 1.f;
+// stats: [G][T][2][C] with the first S rows of every group folded.  Block =
+// 16 channels x 16 row-lanes; lane 0 of each channel walks the groups in order so
+// running stats see G sequential updates.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, int S, int T, int G, int C,
+                                                        long Mg, const float* gamma, const float* beta, float mom,
+                                                        float eps, float* rm, float* rv, float* mean, float* invstd,
+                                                        float* scale, float* shift) {
+  __shared__ double red[256];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
+  float run_m = (lead && rm) ? rm[c] : 0.f, run_v = (lead && rv) ? rv[c] : 1.f;
   for (int g = 0; g < G; ++g) {
     double mu, var;
     if (!stats) {                        // eval mode: running statistics, no update
       mu = run_m;
       var = run_v;
     } else {
-      double s1 = 0.0, s2 = 0.0;
       const float* base = stats + (size_t)g * T * 2 * C;
-      for (int t = 0; t < S; ++t) { s1 += base[(size_t)t * 2 * C + c]; s2 += base[(size_t)t * 2 * C + C + c]; }
+      const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
+      const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
       mu = s1 / Mg;
       var = s2 / Mg - mu * mu;
       if (var < 0) var = 0;
     }
+    if (!lead) continue;
     const float inv = (float)(1.0 / sqrt(var + (double)eps));
     const float sc = gamma[c] * inv;
     mean[g * C + c] = (float)mu;
@@ -76,7 +79,7 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int S, int T
       run_v = (1.f - mom) * run_v + mom * (float)unb;
     }
   }
-  if (rm && stats) { rm[c] = run_m; rv[c] = run_v; }
+  if (lead && rm && stats) { rm[c] = run_m; rv[c] = run_v; }
 }
 
 // ------------------------------------------------------------------ apply
@@ -250,16 +253,19 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
 
 // partial: [G][T][2][C] (first S rows per group folded).  coef: [G][3][C];
 // dgamma/dbeta are summed over groups (one BatchNorm module, G calls).
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int S, int T, int G, int C, long Mg,
-                                       const float* gamma, const float* mean, const float* invstd,
-                                       float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int S, int T, int G,
+                                                            int C, long Mg, const float* gamma, const float* mean,
+                                                            const float* invstd, float* dgamma, float* dbeta,
+                                                            float* coef) {
+  __shared__ double red[256];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
   double dg = 0.0, db = 0.0;
   for (int g = 0; g < G; ++g) {
-    double s1 = 0.0, s2 = 0.0;
     const float* base = partial + (size_t)g * T * 2 * C;
-    for (int t = 0; t < S; ++t) { s1 += base[(size_t)t * 2 * C + c]; s2 += base[(size_t)t * 2 * C + C + c]; }
+    const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
+    const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
+    if (!lead) continue;
     dg += s2;
     db += s1;
     const double is = invstd[g * C + c];
@@ -270,8 +276,8 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int S,
     coef[(size_t)g * 3 * C + C + c] = (float)B;
     coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
   }
-  if (dgamma) dgamma[c] = (float)dg;
-  if (dbeta) dbeta[c] = (float)db;
+  if (lead && dgamma) dgamma[c] = (float)dg;
+  if (lead && dbeta) dbeta[c] = (float)db;
 }
 
 __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restrict__ y, int ycs, long M, int C,
@@ -316,12 +322,14 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restric
 }  // namespace
 
 // sum over tiles of partial[t][C] -> out[C] (fixed order); shared with misc.hip / loss.hip
-__global__ void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int t = 0; t < tiles; ++t) s += partial[(size_t)t * C + c];
-  out[c] = (float)s;
+// launch: grid ceil(C/16), 256 threads (16 channels x 16 row-lanes)
+__global__ __launch_bounds__(256) void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C,
+                                                         float* __restrict__ out) {
+  __shared__ double red[256];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C;
+  const double s = stf::fold16_finish(stf::fold16_partial(partial, tiles, C, c, cok), red);
+  if (cok && (threadIdx.x >> 4) == 0) out[c] = (float)s;
 }
 
 static bool cg_ok(int C) { return C % 8 == 0 && NT % (C / 8) == 0; }
@@ -332,8 +340,8 @@ extern "C" int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64
                                stf_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
-  const int S = stats ? stf::colsum_stage1(stats, tiles, 2L * C, s, groups) : 0;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats, S, tiles, groups, C,
+  const int S = stats ? stf::colsum_stage1(stats, tiles, 2L * C, s, groups, stf::FOLD16_ROWS) : 0;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, stats, S, tiles, groups, C,
                      (long)(M / groups), gamma, beta, momentum, eps, running_mean, running_var, mean, invstd,
                      scale, shift);
   STF_CHECK_LAUNCH();
@@ -403,8 +411,8 @@ extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C,
                                    stf_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
-  const int S = stf::colsum_stage1(partial, tiles, 2L * C, s, groups);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, S, tiles, groups, C,
+  const int S = stf::colsum_stage1(partial, tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, S, tiles, groups, C,
                      (long)(M / groups), gamma, mean, invstd, dgamma, dbeta, coef);
   STF_CHECK_LAUNCH();
   return 0;
@@ -425,8 +433,8 @@ extern "C" int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int
                      y_cstride, (long)M, C, (long)(M / groups), coef, (uint16_t*)dy, dy_cstride, bias_partial);
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
-    const int S = stf::colsum_stage1(bias_partial, tiles, C, s);
-    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias_partial, S, C, dbias);
+    const int S = stf::colsum_stage1(bias_partial, tiles, C, s, 1, stf::FOLD16_ROWS);
+    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(256), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
   return 0;

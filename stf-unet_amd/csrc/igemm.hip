@@ -471,6 +471,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
   const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
+  const int ntiles = a.N * tpi;                         // items: channel slice major, pixel tile minor
+  const int ipg = a.Mg / (a.Hd * a.Wd);                 // images per statistics group
   const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
   const int it0 = blockIdx.x * per + min((int)blockIdx.x, rem);
   const int S = cnt * CC;
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
 
   // live = false: a dummy stage (all lanes out of range) so every iteration issues the same DMA count
   auto issue = [&](int item, int cc, int buf, bool live) {
-    const int nt = item % NTn, tile = item / NTn;
+    const int nt = item / ntiles, tile = item - nt * ntiles;
     const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
     char* st = smem + buf * STAGE;
@@ -528,6 +530,22 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
   issue(it0, 0, 0, true);
   int iit = it0, icc = 0;                               // issue cursor (last issued stage)
   int cit = it0, ccc = 0;                               // compute cursor
+  // BN partial statistics, one row per (group, workgroup): stats [groups][gridDim][2][Nout].
+  // Thread tid < 128 owns (sum | sum of squares, channel col) of the current (group, slice)
+  // and zeroes its rows first (same thread, same addresses: ordered).
+  const int q_st = tid >> 6, col_st = tid & 63;
+  const int groups = a.M / a.Mg;
+  int run_key = -1;
+  float run = 0.f;
+  auto flush = [&]() {
+    const int g = run_key / NTn, nt = run_key - g * NTn;
+    a.stats[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = run;
+  };
+  if (a.stats && tid < 128) {
+    for (int g = 0; g < groups; ++g)
+      for (int nt = 0; nt < NTn; ++nt)
+        a.stats[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = 0.f;
+  }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
   for (int s = 0; s < S; ++s) {
     // retire this stage's DMA; the previous epilogue's 8 buffer stores (issued
@@ -540,7 +558,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
     // that waiting for it never waits for the DMA
     f32x4 bv[TN];
     if (ccc == CC - 1) {
-      const int nt = cit % NTn;
+      const int nt = cit / ntiles;
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         bv[j] = __builtin_amdgcn_raw_buffer_load_b128(rs_bias, (nt * BN + j * 16 + fk * 4) * 4, 0, 0);
@@ -580,7 +598,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
       // issues exactly 8 stores and the next stage can wait with vmcnt(8));
       // BN partial sums from the stored values; raw barriers only, so nothing
       // drains the stores or the DMA already in flight.
-      const int nt = cit % NTn, tile = cit / NTn;
+      const int nt = cit / ntiles, tile = cit - nt * ntiles;
       const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
       char* ot = smem + (s & 1) * STAGE;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -653,7 +671,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
           float t = 0.f;
 #pragma unroll
           for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
-          a.stats[(size_t)tile * 2 * a.Nout + q * a.Nout + nt * BN + col] = t;
+          const int key = (img / ipg) * NTn + nt;
+          if (key != run_key) {
+            if (run_key >= 0) flush();
+            run_key = key;
+            run = 0.f;
+          }
+          run += t;
         }
       }
       ccc = 0;
@@ -661,6 +685,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
       epi = true;
     }
   }
+  if (a.stats && tid < 128 && run_key >= 0) flush();
 }
 
 constexpr int HALO_PH = 16, HALO_PW = 32;
@@ -790,16 +815,20 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
   tx = (c.Wd + HALO_PW - 1) / HALO_PW;
 }
 
+// persistent halo grid: one workgroup per CU (160 KiB LDS each)
+int halo_grid(const stf_igemm_args* a) {
+  int ty, tx;
+  halo_tiles(a->g, ty, tx);
+  const long items = (long)a->g.N * ty * tx * (a->Nout / 64);
+  return (int)std::min<long>(items, num_cus());
+}
+
 // BatchNorm partial-statistics rows per group for the kernel that will run
 int stat_tiles(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
-  if (choose(a, dma_fits(a)) == 'H') {
-    int ty, tx;
-    halo_tiles(c, ty, tx);
-    return (int)(Mg / ((long)c.Hd * c.Wd)) * ty * tx;
-  }
+  if (choose(a, dma_fits(a)) == 'H') return halo_grid(a);
   const int bm = pick_mtile(a);
   return (int)((Mg + bm - 1) / bm);
 }
@@ -842,7 +871,7 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
     int ty, tx;
     halo_tiles(c, ty, tx);
     const long items = (long)c.N * ty * tx * (a->Nout / 64);
-    const int grid = (int)std::min<long>(items, num_cus());
+    const int grid = halo_grid(a);
     static const int diag = [] { const char* e = getenv("STF_HALO_DIAG"); return e ? atoi(e) : 0; }();
 #define STF_H(D) hipLaunchKernelGGL((conv3x3_halo_kernel<HALO_PH, HALO_PW, D>), dim3(grid), dim3(512), 0, s, g, \
                                     src_bytes, ty, tx, (int)(items / grid), (int)(items % grid))

@@ -176,8 +176,8 @@ extern "C" int stf_channel_sum(const void* x, int x_cstride, int M, int C, float
   hipLaunchKernelGGL(channel_sum_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)x, x_cstride, (long)M, C,
                      partial);
   STF_CHECK_LAUNCH();
-  const int S = stf::colsum_stage1(partial, tiles, C, s);
-  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, S, C, out);
+  const int S = stf::colsum_stage1(partial, tiles, C, s, 1, stf::FOLD16_ROWS);
+  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, S, C, out);
   STF_CHECK_LAUNCH();
   return 0;
 }

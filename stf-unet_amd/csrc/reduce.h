@@ -33,12 +33,44 @@ static inline int colsum_split(long T, long W, int G) {
 
 // Fold each group's T rows to S rows in place; returns S (rows per group left,
 // still at group stride T).
-static inline int colsum_stage1(float* buf, long T, long W, hipStream_t st, int G = 1) {
-  if (T <= 8) return (int)T;
+static inline int colsum_stage1(float* buf, long T, long W, hipStream_t st, int G = 1, long min_rows = 8) {
+  if (T <= min_rows) return (int)T;
   const int S = colsum_split(T, W, G);
   if (S >= T) return (int)T;
   hipLaunchKernelGGL(colsum_inplace_kernel, dim3((W + 255) / 256, S, G), dim3(256), 0, st, buf, T, W, S);
   return S;
 }
+
+// Row folding inside one 256-thread block: 16 row-lanes x 16 columns.  Column
+// c = blockIdx.x * 16 + (tid & 15); lane r = tid >> 4 sums rows r, r+16, ... < S
+// of base[t * stride + c] (fp64); fold16_finish returns the total (fixed order)
+// on lane 0.  Consumers (finalize kernels) read <= a few hundred rows this way
+// without a separate folding launch.
+STF_DEV double fold16_partial(const float* base, int S, long stride, int c, bool cok) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;       // four chains: the loads pipeline
+  if (cok) {
+    int t = threadIdx.x >> 4;
+    for (; t + 48 < S; t += 64) {
+      a0 += base[(long)t * stride + c];
+      a1 += base[(long)(t + 16) * stride + c];
+      a2 += base[(long)(t + 32) * stride + c];
+      a3 += base[(long)(t + 48) * stride + c];
+    }
+    for (; t < S; t += 16) a0 += base[(long)t * stride + c];
+  }
+  return (a0 + a1) + (a2 + a3);
+}
+
+STF_DEV double fold16_finish(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  double tot = 0.0;
+  if ((threadIdx.x >> 4) == 0)
+    for (int r = 0; r < 16; ++r) tot += red[r * 16 + (threadIdx.x & 15)];
+  __syncthreads();
+  return tot;
+}
+
+constexpr long FOLD16_ROWS = 1024;    // finalize kernels read up to this many rows directly
 
 }  // namespace stf
