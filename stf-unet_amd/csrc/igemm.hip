@@ -136,6 +136,104 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
 }
 
 
+// LDS-staged epilogue of the linear DMA kernels (EPI 0): the BM x BN tile goes to
+// LDS as bf16(acc + bias) (16-B chunk c of row r at c ^ (r & 7)), then every
+// thread stores whole 16-B chunks of output rows (one fixed 8-channel chunk per
+// thread: full 128-B+ row segments per wave instead of 8-B pieces of 16 rows),
+// adds the old value when accumulating, and sums BN statistics of the stored
+// values.  Needs BM*BN*2 + NW*2*BN*4 bytes of LDS (the drained ring).
+template <int BM, int BN, int WM, int WN, bool SCATTER, int NTH>
+STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end, int n0,
+                             int wm, int wn, int tid, char* smem, int tile) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int CPR = BN / 8, RPP = NTH / CPR, PASSES = BM / RPP, NW = WM * WN;
+  static_assert(NTH % CPR == 0 && BM % RPP == 0, "epilogue mapping");
+  const int lane = tid & 63, fr = lane & 15, fk = lane >> 4, wave = tid >> 6;
+  const int Cout = SCATTER ? a.Nout / 4 : a.Nout;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WTN + j * 16 + fk * 4;           // tile column of this lane's 4 channels
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && n0 + nl < a.Nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = a.bias[SCATTER ? (n0 + nl + r) % Cout : n0 + nl + r];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + fr;
+      const uint2 v = make_uint2(pack2(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1]),
+                                 pack2(acc[i][j][2] + bv[2], acc[i][j][3] + bv[3]));
+      *reinterpret_cast<uint2*>(smem + row * (BN * 2) + (((nl >> 3) ^ (row & 7)) << 4) + (nl & 7) * 2) = v;
+    }
+  }
+  __syncthreads();
+  const int c = tid % CPR, n = n0 + c * 8;
+  const bool nok = n < a.Nout;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll 4
+  for (int ps = 0; ps < PASSES; ++ps) {
+    const int row = tid / CPR + ps * RPP;
+    const int m = m0 + row;
+    if (!(nok && m < m_end)) continue;
+    uint4 u = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((c ^ (row & 7)) << 4));
+    size_t off;
+    if (SCATTER) {
+      const int blk = n / Cout, co = n - blk * Cout;
+      const int hw = a.Hd * a.Wd;
+      const int img = m / hw, rem = m - img * hw;
+      const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+      off = ((size_t)(img * 2 * a.Hd + 2 * yd + (blk >> 1)) * (2 * a.Wd) + 2 * xd + (blk & 1)) * a.dcs + co;
+    } else {
+      off = (size_t)m * a.dcs + n;
+    }
+    float f[8];
+    unpack8(u, f);
+    if (a.accumulate) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.dst + off), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = round_bf(f[e] + o[e]);
+      u = pack8(f);
+    }
+    *reinterpret_cast<uint4*>(a.dst + off) = u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
+  }
+  if (a.stats == nullptr) return;
+  // threads with equal c: fold within the wave (lanes c, c+CPR, ...), then over waves
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  float* red = reinterpret_cast<float*>(smem + BM * BN * 2);   // [NW][2][BN]
+  constexpr int CW = CPR < 64 ? CPR : 64;                       // distinct chunks per wave
+  if (lane < CW) {
+    const int cc = (wave * 64 + lane) % CPR;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(wave * 2 + 0) * BN + cc * 8 + e] = s1[e];
+      red[(wave * 2 + 1) * BN + cc * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  // chunk cc appears in the waves whose 64 lanes cover it
+  for (int col = tid; col < 2 * BN; col += NTH) {
+    const int q = col / BN, cl = col - q * BN, cc = cl >> 3;
+    if (n0 + cl >= a.Nout) continue;
+    float t = 0.f;
+    for (int w = 0; w < NW; ++w) {
+      const int first = (w * 64) % CPR;                         // chunks held by wave w: first .. first+CW-1 (mod CPR)
+      if (((cc - first + CPR) % CPR) < CW) t += red[(w * 2 + q) * BN + cl];
+    }
+    a.stats[(size_t)tile * 2 * a.Nout + q * a.Nout + n0 + cl] = t;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool SMALLC, bool TRANS, bool SCATTER, int EPI>
 __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
   constexpr int WTM = BM / WM, WTN = BN / WN;     // wave tile (pixels x channels)
@@ -306,7 +404,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   constexpr int RPI = 64 / CPR;                         // rows per DMA wave-instruction (1 KiB)
   constexpr int LA = BM / NW / RPI, LB = BN / NW / RPI; // DMA instructions per wave per K step
   constexpr int STAGE = (BM + BN) * ROWB;
-  constexpr int LDS_MAIN = STAGES * STAGE, LDS_RED = WM * 2 * BN * 4;
+  constexpr int LDS_MAIN = STAGES * STAGE;
+  constexpr int LDS_RED = EPI == 0 ? BM * BN * 2 + NW * 2 * BN * 4 : WM * 2 * BN * 4;
   static_assert(LA >= 1 && LB >= 1 && LA * RPI * NW == BM && LB * RPI * NW == BN, "tile");
   __shared__ __attribute__((aligned(16))) char smem[LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED];
 
@@ -426,13 +525,17 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  int mrow[TM];
+  if constexpr (EPI == 0) {
+    staged_epilogue<BM, BN, WM, WN, SCATTER, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx);
+  } else {
+    int mrow[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WTM + i * 16 + fr;
-    mrow[i] = m < m_end ? m : -1;
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      mrow[i] = m < m_end ? m : -1;
+    }
+    igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NTH>(a, acc, mrow, n0, wm, wn, tid, smem, bx);
   }
-  igemm_epilogue<BM, BN, WM, WN, SCATTER, EPI, NTH>(a, acc, mrow, n0, wm, wn, tid, smem, bx);
 }
 
 
@@ -740,9 +843,9 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   if (f == '0' && halo_ok && c.Wd >= 32) return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
-    if (plain && bk64) return f;
+    if ((plain || a->scatter2x2) && bk64 && !a->lstm && !c.transposed) return f;
   }
-  if (plain && bk64) {
+  if ((plain || (a->scatter2x2 && !c.transposed && !a->lstm)) && bk64) {
     // measured per layer (tools/bench_layers.py, cfg2 shapes): C where it fills the chip,
     // B for 128-multiples, D for 64 output channels
     const long M = (long)c.N * c.Hd * c.Wd;
@@ -777,11 +880,16 @@ void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, uint32_t src_
 #undef STF_D
 }
 
+// plain forward gather (or its ConvT 2x2 scatter epilogue) on the 8-wave tiles
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
-void launch_dma_plain(const Geo& g, uint32_t src_bytes, hipStream_t s) {
+void launch_dma_plain(const Geo& g, bool scatter, uint32_t src_bytes, hipStream_t s) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
-  hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 0>), grid, block, 0, s, g,
-                     src_bytes);
+  if (scatter)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, true, 0>), grid, block, 0, s, g,
+                       src_bytes);
+  else
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 0>), grid, block, 0, s, g,
+                       src_bytes);
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -883,9 +991,9 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   switch (k) {
     case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
     case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
-    case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, src_bytes, s); break;
-    case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, src_bytes, s); break;
-    case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, src_bytes, s); break;
+    case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, a->scatter2x2, src_bytes, s); break;
+    case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, a->scatter2x2, src_bytes, s); break;
+    case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, a->scatter2x2, src_bytes, s); break;
     default:
       if (bm == 256) return launch_reg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
       return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);

@@ -58,3 +58,29 @@ for name, h, ci, co in layers:
           f"  dgrad {td:7.3f} ms {flops/td/1e9:7.1f} TF  wgrad {tw:7.3f} ms {flops/tw/1e9:7.1f} TF", flush=True)
 for k, (t, f) in tot.items():
     print(f"TOTAL {k}: {t:.2f} ms  {f/t/1e9:.1f} TF/s")
+
+# ConvTranspose2d(k=2, s=2) of the decoder: forward (scatter epilogue into the concat
+# half), input gradient (stride-2 2x2 gather) and weight gradient
+tot = [0, 0, 0, 0]
+for h, cin in ((16, 1024), (32, 512), (64, 256), (128, 128)):
+    cout = cin // 2
+    x = nhwc.new_feat(B, h, h, cin, dev)
+    x.buf.normal_()
+    cat = nhwc.new_feat(B, 2 * h, 2 * h, 2 * cout, dev)
+    cat.buf.normal_()
+    w = torch.randn(cin, cout, 2, 2, device=dev) * 0.05
+    b = torch.randn(cout, device=dev)
+    w2 = nhwc.pack_weight(w, 2)
+    w3 = nhwc.pack_weight(w, 3)
+    flops = 2.0 * B * h * h * cin * 4 * cout
+    up = cat.slice(0, cout)
+    tf = timeit(lambda: nhwc.igemm(x, w2, 4 * cout, up, 1, 1, 1, 0, bias=b, scatter2x2=True))
+    dy = nhwc.new_feat(B, 2 * h, 2 * h, cout, dev)
+    dy.buf.normal_()
+    td = timeit(lambda: nhwc.igemm(dy, w3, cin, x, 2, 2, 2, 0))
+    out = torch.empty(cin * cout * 4, device=dev)
+    tw = timeit(lambda: nhwc.wgrad(x, dy, 2, 2, 2, 0, out))
+    print(f"up{h:<5d} {h:4d}^2 {cin:5d}->{cout:5d}  GF {flops/1e9:8.1f}  fwd {tf:7.3f} ms {flops/tf/1e9:7.1f} TF"
+          f"  dgrad {td:7.3f} ms {flops/td/1e9:7.1f} TF  wgrad {tw:7.3f} ms {flops/tw/1e9:7.1f} TF", flush=True)
+    tot[0] += tf; tot[1] += td; tot[2] += tw; tot[3] += flops
+print(f"TOTAL convT: fwd {tot[0]:.2f} ms dgrad {tot[1]:.2f} ms wgrad {tot[2]:.2f} ms")
