@@ -227,10 +227,13 @@ int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int 
  * x[b][T+p][0] (src/stf_lstm_unet.py:146-156,172-174), rest zero. */
 int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int T, int P,
                       int Cpad, void* out, stf_stream_t stream);
-/* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16;
- * backward gathers dout over the windows whose first maximum is the pixel. */
-int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, stf_stream_t stream);
-int stf_maxpool3s2_bwd(const void* x, const void* dout, int N, int H, int W, int C, void* dx,
+/* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16.
+ * argmax (uint8 [N][Ho][Wo][C], NULL in eval) records each window's first maximum
+ * (index dy*3+dx, torch's tie rule); backward gathers dout over the <= 4 windows
+ * whose recorded maximum is the pixel. */
+int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, void* argmax,
+                       stf_stream_t stream);
+int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W, int C, void* dx,
                        stf_stream_t stream);
 /* nn.LSTM(C, C) weights -> gate-interleaved GEMM operands: wcat [4C][2C] (row
  * 4c+q = torch row q*C+c of [W_ih | W_hh]), wcat_t [2C][4C], bias = b_ih + b_hh

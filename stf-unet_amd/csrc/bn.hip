@@ -42,44 +42,63 @@ int tiles_per_group(long units_per_group, int groups) {
 }
 
 // ------------------------------------------------------------------ finalize
-// stats: [G][T][2][C] with the first S rows of every group folded.  Block =
-// 16 channels x 16 row-lanes; lane 0 of each channel walks the groups in order so
-// running stats see G sequential updates.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, int S, int T, int G, int C,
+// stats: [G][T][2][C] with the first S rows of every group folded.  Grid =
+// (channel chunks of 16) x G; block = 16 channels x 16 row-lanes folding ONE
+// group.  With G > 1 the running statistics must see the G updates in order:
+// each block parks (mean, biased var) in row 0 of its group (scratch) and
+// bn_running_kernel applies them sequentially.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(float* __restrict__ stats, int S, int T, int G, int C,
                                                         long Mg, const float* gamma, const float* beta, float mom,
                                                         float eps, float* rm, float* rv, float* mean, float* invstd,
                                                         float* scale, float* shift) {
   __shared__ double red[256];
+  const int g = blockIdx.y;
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
-  float run_m = (lead && rm) ? rm[c] : 0.f, run_v = (lead && rv) ? rv[c] : 1.f;
-  for (int g = 0; g < G; ++g) {
-    double mu, var;
-    if (!stats) {                        // eval mode: running statistics, no update
-      mu = run_m;
-      var = run_v;
-    } else {
-      const float* base = stats + (size_t)g * T * 2 * C;
-      const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
-      const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
-      mu = s1 / Mg;
-      var = s2 / Mg - mu * mu;
-      if (var < 0) var = 0;
-    }
-    if (!lead) continue;
-    const float inv = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * inv;
-    mean[g * C + c] = (float)mu;
-    invstd[g * C + c] = inv;
-    scale[g * C + c] = sc;
-    shift[g * C + c] = beta[c] - (float)mu * sc;
-    if (rm && stats) {
-      run_m = (1.f - mom) * run_m + mom * (float)mu;
-      const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
-      run_v = (1.f - mom) * run_v + mom * (float)unb;
-    }
+  double mu = 0.0, var = 1.0;
+  float* base = stats ? stats + (size_t)g * T * 2 * C : nullptr;
+  if (stats) {
+    const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
+    const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
+    mu = s1 / Mg;
+    var = s2 / Mg - mu * mu;
+    if (var < 0) var = 0;
+  } else if (lead) {                     // eval mode: running statistics, no update
+    mu = rm ? rm[c] : 0.f;
+    var = rv ? rv[c] : 1.f;
   }
-  if (lead && rm && stats) { rm[c] = run_m; rv[c] = run_v; }
+  if (!lead) return;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * inv;
+  mean[g * C + c] = (float)mu;
+  invstd[g * C + c] = inv;
+  scale[g * C + c] = sc;
+  shift[g * C + c] = beta[c] - (float)mu * sc;
+  if (!(rm && stats)) return;
+  if (G == 1) {
+    const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
+    rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
+    rv[c] = (1.f - mom) * rv[c] + mom * (float)unb;
+  } else {
+    base[c] = (float)mu;
+    base[C + c] = (float)var;
+  }
+}
+
+__global__ void bn_running_kernel(const float* __restrict__ stats, int T, int G, int C, long Mg, float mom,
+                                  float* rm, float* rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float run_m = rm[c], run_v = rv[c];
+  for (int g = 0; g < G; ++g) {
+    const float* base = stats + (size_t)g * T * 2 * C;
+    const double var = base[C + c];
+    const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
+    run_m = (1.f - mom) * run_m + mom * base[c];
+    run_v = (1.f - mom) * run_v + mom * (float)unb;
+  }
+  rm[c] = run_m;
+  rv[c] = run_v;
 }
 
 // ------------------------------------------------------------------ apply
@@ -251,33 +270,50 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
   }
 }
 
-// partial: [G][T][2][C] (first S rows per group folded).  coef: [G][3][C];
-// dgamma/dbeta are summed over groups (one BatchNorm module, G calls).
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ partial, int S, int T, int G,
+// partial: [G][T][2][C] (first S rows per group folded).  coef: [G][3][C].
+// Grid = (channel chunks of 16) x G.  dgamma/dbeta are summed over the groups
+// (one BatchNorm module, G calls): with G > 1 each block parks its group's sums
+// in row 0 of the group and bn_bwd_groupsum_kernel adds them in order.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
                                                             int C, long Mg, const float* gamma, const float* mean,
                                                             const float* invstd, float* dgamma, float* dbeta,
                                                             float* coef) {
   __shared__ double red[256];
+  const int g = blockIdx.y;
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
+  float* base = partial + (size_t)g * T * 2 * C;
+  const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
+  const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
+  if (!lead) return;
+  const double is = invstd[g * C + c];
+  const double A = (double)gamma[c] * is;
+  const double B = -A * is * s2 / Mg;
+  const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
+  coef[(size_t)g * 3 * C + c] = (float)A;
+  coef[(size_t)g * 3 * C + C + c] = (float)B;
+  coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
+  if (G == 1) {
+    if (dgamma) dgamma[c] = (float)s2;
+    if (dbeta) dbeta[c] = (float)s1;
+  } else {
+    base[c] = (float)s1;
+    base[C + c] = (float)s2;
+  }
+}
+
+__global__ void bn_bwd_groupsum_kernel(const float* __restrict__ partial, int T, int G, int C, float* dgamma,
+                                       float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
   double dg = 0.0, db = 0.0;
   for (int g = 0; g < G; ++g) {
     const float* base = partial + (size_t)g * T * 2 * C;
-    const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
-    const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
-    if (!lead) continue;
-    dg += s2;
-    db += s1;
-    const double is = invstd[g * C + c];
-    const double A = (double)gamma[c] * is;
-    const double B = -A * is * s2 / Mg;
-    const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
-    coef[(size_t)g * 3 * C + c] = (float)A;
-    coef[(size_t)g * 3 * C + C + c] = (float)B;
-    coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
+    db += base[c];
+    dg += base[C + c];
   }
-  if (lead && dgamma) dgamma[c] = (float)dg;
-  if (lead && dbeta) dbeta[c] = (float)db;
+  if (dgamma) dgamma[c] = (float)dg;
+  if (dbeta) dbeta[c] = (float)db;
 }
 
 __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restrict__ y, int ycs, long M, int C,
@@ -341,10 +377,15 @@ extern "C" int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
   const int S = stats ? stf::colsum_stage1(stats, tiles, 2L * C, s, groups, stf::FOLD16_ROWS) : 0;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, stats, S, tiles, groups, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, stats, S, tiles, groups, C,
                      (long)(M / groups), gamma, beta, momentum, eps, running_mean, running_var, mean, invstd,
                      scale, shift);
   STF_CHECK_LAUNCH();
+  if (stats && running_mean && groups > 1) {
+    hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, s, stats, tiles, groups, C,
+                       (long)(M / groups), momentum, running_mean, running_var);
+    STF_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -412,9 +453,14 @@ extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C,
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
   const int S = stf::colsum_stage1(partial, tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, S, tiles, groups, C,
-                     (long)(M / groups), gamma, mean, invstd, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, partial, S, tiles, groups,
+                     C, (long)(M / groups), gamma, mean, invstd, dgamma, dbeta, coef);
   STF_CHECK_LAUNCH();
+  if (groups > 1 && (dgamma || dbeta)) {
+    hipLaunchKernelGGL(bn_bwd_groupsum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, tiles, groups, C,
+                       dgamma, dbeta);
+    STF_CHECK_LAUNCH();
+  }
   return 0;
 }
 

@@ -43,7 +43,7 @@ __global__ void pack_sequence_kernel(const float* __restrict__ x, int B, int Tto
 
 // MaxPool2d(k=3, s=2, p=1); first maximum in row-major window order (torch CPU)
 __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo,
-                                    uint16_t* __restrict__ out) {
+                                    uint16_t* __restrict__ out, uint8_t* __restrict__ argmax) {
   const int CG = C / 8;
   const long units = (long)N * Ho * Wo * CG;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
@@ -53,8 +53,9 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int oy = rem / Wo, ox = rem - oy * Wo;
     float mx[8];
+    int am[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mx[j] = -INFINITY;
+    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = -1; }
     for (int dy = 0; dy < 3; ++dy) {
       const int iy = 2 * oy - 1 + dy;
       if (iy < 0 || iy >= H) continue;
@@ -64,17 +65,24 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
         float v[8];
         unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + iy) * W + ix) * C + cg * 8), v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) mx[j] = v[j] > mx[j] ? v[j] : mx[j];
+        for (int j = 0; j < 8; ++j)          // first maximum in scan order (torch's index)
+          if (v[j] > mx[j] || am[j] < 0) { mx[j] = v[j]; am[j] = dy * 3 + dx; }
       }
     }
     *reinterpret_cast<uint4*>(out + p * C + cg * 8) = pack8(mx);
+    if (argmax) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[4 + j] << (8 * j); }
+      *reinterpret_cast<uint2*>(argmax + p * C + cg * 8) = make_uint2(lo, hi);
+    }
   }
 }
 
 // gather form of the backward: every input pixel sums dout over the (<= 4)
-// windows whose recomputed argmax is this pixel -- no atomics, deterministic
-__global__ void maxpool3_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dout, int N, int H,
-                                    int W, int C, int Ho, int Wo, uint16_t* __restrict__ dx) {
+// windows whose recorded first maximum is this pixel -- no atomics, fixed order
+__global__ void maxpool3_bwd_kernel(const uint8_t* __restrict__ argmax, const uint16_t* __restrict__ dout, int N,
+                                    int H, int W, int C, int Ho, int Wo, uint16_t* __restrict__ dx) {
   const int CG = C / 8;
   const long units = (long)N * H * W * CG;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
@@ -87,29 +95,16 @@ __global__ void maxpool3_bwd_kernel(const uint16_t* __restrict__ x, const uint16
     // windows containing iy: 2*oy-1 <= iy <= 2*oy+1  <=>  iy/2 <= oy <= (iy+1)/2
     for (int oy = iy / 2; oy <= min(Ho - 1, (iy + 1) / 2); ++oy) {
       for (int ox = ix / 2; ox <= min(Wo - 1, (ix + 1) / 2); ++ox) {
-        float best[8];
-        int arg[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = -1; }
-        for (int dy = 0; dy < 3; ++dy) {
-          const int yy = 2 * oy - 1 + dy;
-          if (yy < 0 || yy >= H) continue;
-          for (int dxw = 0; dxw < 3; ++dxw) {
-            const int xx = 2 * ox - 1 + dxw;
-            if (xx < 0 || xx >= W) continue;
-            float v[8];
-            unpack8(*reinterpret_cast<const uint4*>(x + (((long)n * H + yy) * W + xx) * C + cg * 8), v);
-            const int id = yy * W + xx;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (v[j] > best[j] || arg[j] < 0) { best[j] = v[j]; arg[j] = id; }
-          }
-        }
+        const long wo = (((long)n * Ho + oy) * Wo + ox) * C + cg * 8;
+        const uint2 am = *reinterpret_cast<const uint2*>(argmax + wo);
+        const uint32_t me = (uint32_t)((iy - 2 * oy + 1) * 3 + (ix - 2 * ox + 1));
         float d[8];
-        unpack8(*reinterpret_cast<const uint4*>(dout + (((long)n * Ho + oy) * Wo + ox) * C + cg * 8), d);
-        const int me = iy * W + ix;
+        unpack8(*reinterpret_cast<const uint4*>(dout + wo), d);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) if (arg[j] == me) acc[j] += d[j];
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t a = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
+          if (a == me) acc[j] += d[j];
+        }
       }
     }
     *reinterpret_cast<uint4*>(dx + p * C + cg * 8) = pack8(acc);
@@ -214,23 +209,24 @@ extern "C" int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, 
   return 0;
 }
 
-extern "C" int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, stf_stream_t stream) {
+extern "C" int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, void* argmax,
+                                  stf_stream_t stream) {
   if (C % 8) return STF_EINVAL;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long units = (long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
-                     (const uint16_t*)x, N, H, W, C, Ho, Wo, (uint16_t*)out);
+                     (const uint16_t*)x, N, H, W, C, Ho, Wo, (uint16_t*)out, (uint8_t*)argmax);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int stf_maxpool3s2_bwd(const void* x, const void* dout, int N, int H, int W, int C, void* dx,
+extern "C" int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W, int C, void* dx,
                                   stf_stream_t stream) {
   if (C % 8) return STF_EINVAL;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long units = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
-                     (const uint16_t*)x, (const uint16_t*)dout, N, H, W, C, Ho, Wo, (uint16_t*)dx);
+                     (const uint8_t*)argmax, (const uint16_t*)dout, N, H, W, C, Ho, Wo, (uint16_t*)dx);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -219,8 +219,20 @@ class BNState:
         return st
 
 
+# num_batches_tracked increments are deferred and applied per forward with one
+# multi-tensor launch per increment value (instead of one tiny kernel per module)
+_NBT_PENDING = {}
+
+
+def flush_batches_tracked():
+    for inc, ts in _NBT_PENDING.items():
+        torch._foreach_add_(ts, inc)
+    _NBT_PENDING.clear()
+
+
 def bn_finalize(stats, tiles, bn, M, training, groups=1):
-    """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats."""
+    """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats (its
+    num_batches_tracked advances by ``groups`` at flush_batches_tracked())."""
     C = bn.num_features
     st = BNState(C, bn.weight.device, M, groups)
     mom = 0.1 if bn.momentum is None else bn.momentum
@@ -231,7 +243,7 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
          _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
          stream())
     if training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(groups)
+        _NBT_PENDING.setdefault(groups, []).append(bn.num_batches_tracked)
     return st
 
 

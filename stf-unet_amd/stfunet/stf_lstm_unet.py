@@ -256,6 +256,7 @@ class STFProgram:
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
         m = self.m
+        nhwc._NBT_PENDING.clear()
         dev = x.device
         B, Ttot, Cf, H, W = x.shape
         P = m.pk_channels if m.use_pk_maps else 0
@@ -278,7 +279,8 @@ class STFProgram:
         nhwc.bn_act(y0, S.bn0, a0)
         h4, w4 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
         p0 = new_feat(N, h4, w4, 64, dev)
-        call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), stream())
+        S.pool_arg = torch.empty(N * h4 * w4 * 64, dtype=torch.uint8, device=dev) if training else None
+        call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), _p(S.pool_arg), stream())
         S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
         # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat)
         S.enc, S.lbuf, S.pkbuf = [], [], []
@@ -357,6 +359,7 @@ class STFProgram:
         S.head_w = m.final.weight.detach().reshape(K, -1).contiguous()
         call("stf_head_fwd", fr_out.ptr(), B, u1.H, u1.W, fr_out.C, _p(S.ident.scale), _p(S.ident.shift),
              _p(S.head_w), _p(m.final.bias.detach()), K, _p(logits), stream())
+        nhwc.flush_batches_tracked()
         return logits, (S if need_bwd else None)
 
     # ------------------------------------------------------------------ backward
@@ -430,7 +433,7 @@ class STFProgram:
             self._done(getattr(m, f"layer{li + 1}"))
         # stem: maxpool(3,2,1) <- relu(bn1(conv1 x))
         da0 = new_feat(S.a0.N, S.a0.H, S.a0.W, 64, dev)
-        call("stf_maxpool3s2_bwd", S.a0.ptr(), dout.ptr(), S.a0.N, S.a0.H, S.a0.W, 64, da0.ptr(), stream())
+        call("stf_maxpool3s2_bwd", _p(S.pool_arg), dout.ptr(), S.a0.N, S.a0.H, S.a0.W, 64, da0.ptr(), stream())
         dy0 = nhwc.bn_backward(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), dz=da0)
         cin = m.conv1.in_channels
         if S.xin.C == cin:

@@ -121,6 +121,7 @@ class UNetProgram:
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
         m = self.m
+        nhwc._NBT_PENDING.clear()
         N, _, H, W = x.shape
         assert H % 16 == 0 and W % 16 == 0, "UNet needs H, W divisible by 16 (four 2x2 pools)"
         dev = x.device
@@ -164,6 +165,7 @@ class UNetProgram:
                   nhwc._p(S.head_w), nhwc._p(m.out_conv.bias.detach()), K, nhwc._p(logits), nhwc.stream())
         if not need_bwd:
             S.enc = S.cats = S.dec = None
+        nhwc.flush_batches_tracked()
         return logits, (S if need_bwd else None)
 
     # ------------------------------------------------------------------ backward

@@ -89,6 +89,7 @@ def test_basic_block_grouped_bn(cin, cout, stride, groups):
     src = feat_from(x)
     out = nhwc.new_feat(groups * B, H // stride, H // stride, cout, DEV)
     s = prog.forward(src, out, True, groups)
+    nhwc.flush_batches_tracked()                     # what the model programs do after forward
     gv = _Grads(blk)
     dsrc = prog.backward(s, gv, dout=feat_from(R))
     # torch reference: one BN batch per group, running stats advanced per group in order
@@ -162,19 +163,24 @@ def test_lstm_component(C, T):
 
 
 def test_maxpool3_fwd_bwd():
+    """MaxPool2d(3,2,1) incl. ties (bf16 values repeat): the recorded first maximum
+    must route the gradient exactly like torch."""
     from stfunet import nhwc
     from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
     x = bfr(torch.randn(2, 64, 15, 16, device=DEV))
+    x[:, :8] = torch.round(x[:, :8])                       # many ties in the first channels
     xr = x.clone().requires_grad_(True)
     ref = F.max_pool2d(xr, 3, 2, 1)
     xf = feat_from(x)
     out = nhwc.new_feat(2, ref.shape[2], ref.shape[3], 64, DEV)
-    call("stf_maxpool3s2_fwd", xf.ptr(), 2, 15, 16, 64, out.ptr(), stream())
+    arg = torch.empty(2 * ref.shape[2] * ref.shape[3] * 64, dtype=torch.uint8, device=DEV)
+    call("stf_maxpool3s2_fwd", xf.ptr(), 2, 15, 16, 64, out.ptr(), _p(arg), stream())
     assert torch.equal(out.dense(), ref.detach())
     d = bfr(torch.randn_like(ref))
     ref.backward(d)
     dx = nhwc.new_feat(2, 15, 16, 64, DEV)
-    call("stf_maxpool3s2_bwd", xf.ptr(), feat_from(d).ptr(), 2, 15, 16, 64, dx.ptr(), stream())
+    call("stf_maxpool3s2_bwd", _p(arg), feat_from(d).ptr(), 2, 15, 16, 64, dx.ptr(), stream())
     assert rel(dx.dense(), xr.grad) < 1e-2
 
 
