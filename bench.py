@@ -52,6 +52,42 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(kernel, workload, batch):
+    """HBM bytes per launch of ``kernel`` from the committed PMC passes
+    (tools/pmc_passes.sh + tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE) of the
+    same workload; None when no matching measurement is committed."""
+    path = os.path.join(HERE, "profiles", "r01", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("workload") != workload or d.get("batch") != batch:
+        return None, None
+    k = d.get("kernels", {}).get(kernel)
+    return (k["hbm_bytes_per_launch"], os.path.relpath(path, HERE)) if k else (None, None)
+
+
+def roofline(kt, workload, batch):
+    """Roofline of the dominant kernel (largest summed time in the timed region,
+    HIP events on its launch stream): algorithmic FLOPs per launch (2*M*N*K) over
+    its average launch duration, against the dense bf16 MFMA peak."""
+    if not kt:
+        return None
+    name = max(kt, key=lambda k: kt[k]["ms"])
+    k = kt[name]
+    traffic, src = pmc_traffic(name, workload, batch)
+    gemm_ms = sum(v["ms"] for v in kt.values())
+    gemm_fl = sum(v["flops"] for v in kt.values())
+    return {"bound": "mfma", "kernel": name, "achieved": round(k["tflops"], 2), "peak": MFMA_BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC 2*FETCH_SIZE+WRITE_SIZE)",
+            "traffic_source": src, "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
+            "algorithmic_tflop_per_launch": round(k["flops"] / k["launches"] / 1e12, 6),
+            "all_conv_gemm_kernels": {"ms": round(gemm_ms, 3),
+                                      "tflops": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else 0.0}}
+
+
 def cpu_baseline(args):
     """fp32 oracle (plain PyTorch CPU restatement of src/unet.py or
     src/stf_lstm_unet.py + criterion + AdamW) on a bounded sample: B=2 at the
@@ -178,25 +214,18 @@ def main():
         else:
             from oracle.stf import train_flops_per_sample
             train_gflop = train_flops_per_sample(args.time_steps, args.size, args.size, args.pk) / 1e9
-        roof = None
-        if "igemm" in kt:
-            k = kt["igemm"]
-            per_launch = k["flops"] / k["launches"] / 1e12
-            roof = {"bound": "mfma", "kernel": "stf_igemm (conv fwd + dgrad + convT, all launches)",
-                    "achieved": round(k["tflops"], 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
-                    "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
-                    "avg_algorithmic_tflop_per_launch": round(per_launch, 6)}
+        workload = (f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
+                    if args.model == "unet" else
+                    f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
+                    f"{args.size}x{args.size} train step")
+        roof = roofline(kt, workload, args.batch)
         res = {
             "metric": "training samples/sec (256x256 DCE-MRI frames)",
             "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
-            "config": {"workload": (f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
-                                    if args.model == "unet" else
-                                    f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
-                                    f"{args.size}x{args.size} train step"),
+            "config": {"workload": workload,
                        "model": "UNet" if args.model == "unet" else "STFLSTMUNet",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": args.time_steps, "image": [args.size, args.size],

@@ -84,6 +84,9 @@ typedef struct stf_igemm_args {
 /* Partial-statistics rows per group for these args (the tiling depends on the
  * kernel chosen): size `stats` as groups * stf_igemm_stat_tiles(a) * 2 * Nout. */
 int stf_igemm_stat_tiles(const stf_igemm_args* a);
+/* Device kernel (template instance, as rocprofv3 names it) these args will run;
+ * static thread-local string, for per-kernel timers and profile cross-checks. */
+const char* stf_igemm_kernel_name(const stf_igemm_args* a);
 /* Conv2d 3x3/1x1/strided forward with fused bias + BatchNorm partial statistics
  *   replaces nn.Conv2d in conv_block  (src/unet.py:12,15), ResidualConvBlock
  *   (src/stf_lstm_unet.py:13,16,23), ResNet-34 convs (src/stf_lstm_unet.py:108-114),
@@ -109,6 +112,8 @@ int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_bytes);
 /* dW[n][r][s][c] partials = sum over pixels dy[m][n] * x[gather(m,r,s)][c]
  *   replaces the weight gradient of every Conv2d/ConvTranspose2d above. */
 int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream);
+/* Device kernel stf_wgrad runs for these args (see stf_igemm_kernel_name). */
+const char* stf_wgrad_kernel_name(const stf_wgrad_args* a);
 /* Sum `splits` slabs into out[Nout][Cs][R][S] (PyTorch Conv2d weight layout;
  * for ConvTranspose2d pass Nout=Cin, Cs=Cout and get [Cin][Cout][R][S]).
  * Partial-slab arguments of this and the *_finalize / channel-sum functions are

@@ -14,6 +14,7 @@
 // makes the ds_read_b128 fragment reads conflict-free for all four lane groups.
 #include "common.h"
 #include "../../include/stfunet.h"
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace {
@@ -944,6 +945,30 @@ int stat_tiles(const stf_igemm_args* a) {
 }  // namespace
 
 extern "C" int stf_igemm_stat_tiles(const stf_igemm_args* a) { return stat_tiles(a); }
+
+// Name of the device kernel these args run (as rocprofv3 prints it), for timers
+extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
+  static thread_local char buf[128];
+  const stf_conv_geom& c = a->g;
+  const char k = choose(a, dma_fits(a));
+  const int epi = a->lstm ? 1 : 0;
+  const char* tr = c.transposed ? "true" : "false";
+  const char* sc = a->scatter2x2 ? "true" : "false";
+  switch (k) {
+    case 'H': snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%d, %d, 0>", HALO_PH, HALO_PW); break;
+    case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d>", tr, sc, epi); break;
+    case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d>", tr, sc, epi); break;
+    case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, 0>", sc); break;
+    case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, 0>", sc); break;
+    case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, 0>", sc); break;
+    default: {
+      const bool small = (a->Nout <= 64 && !a->lstm);
+      snprintf(buf, sizeof buf, "igemm_kernel<%s, %s, %s, %s, %d>", small ? "256, 64, 4, 1" : "128, 128, 2, 2",
+               (c.Cs % BK) ? "true" : "false", tr, sc, epi);
+    }
+  }
+  return buf;
+}
 
 extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
   const stf_conv_geom& c = a->g;

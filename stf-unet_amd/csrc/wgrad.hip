@@ -372,6 +372,12 @@ extern "C" int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_b
   return 0;
 }
 
+extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
+  if (const int pw = fused_pw(a)) return pw == 16 ? "wgrad3x3_kernel<16>" : "wgrad3x3_kernel<8>";
+  if (big_tile(a)) return "wgrad_kernel<128, 128, 32, false>";
+  return a->g.Cs % 64 == 0 ? "wgrad_kernel<64, 64, 64, false>" : "wgrad_kernel<64, 64, 64, true>";
+}
+
 extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   const stf_conv_geom& c = a->g;
   if (c.transposed || a->Nout % 8 || c.Cs % 8 || a->dy_cstride % 8 || c.src_cstride % 8) return STF_EINVAL;

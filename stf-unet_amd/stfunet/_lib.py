@@ -41,6 +41,8 @@ class WgradArgs(ctypes.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "stf_igemm_stat_tiles": (c_int, [ctypes.POINTER(IgemmArgs)]),
+    "stf_igemm_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(IgemmArgs)]),
+    "stf_wgrad_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(WgradArgs)]),
     "stf_igemm": (c_int, [ctypes.POINTER(IgemmArgs), P]),
     "stf_wgrad_plan": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_size_t)]),
     "stf_wgrad": (c_int, [ctypes.POINTER(WgradArgs), P]),

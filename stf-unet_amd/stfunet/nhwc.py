@@ -151,7 +151,8 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     call("stf_igemm", ctypes.byref(a), stream())
     if t is not None:
         macs = src.N * Hd * Wd * nout * R * S * src.C
-        t.end(ev, "igemm", 2.0 * macs / (stride * stride if transposed else 1))
+        name = _lib.load().stf_igemm_kernel_name(ctypes.byref(a)).decode()
+        t.end(ev, name, 2.0 * macs / (stride * stride if transposed else 1))
     return stats, tiles
 
 
@@ -187,7 +188,7 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
     ev = t.begin() if t is not None else None
     call("stf_wgrad", ctypes.byref(a), stream())
     if t is not None:
-        t.end(ev, "wgrad", 2.0 * dy.M * dy.C * R * S * x.C)
+        t.end(ev, _lib.load().stf_wgrad_kernel_name(ctypes.byref(a)).decode(), 2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad_reduce", _p(ws), splits.value, dy.C, R, S, x.C, _p(out), stream())
 
 
