@@ -139,11 +139,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # STF_DIST_BACKEND=gloo (+ ranks sharing one GPU, device = local rank mod
+    # device count) rehearses the N > 1 path on a one-GPU box; the driver's
+    # multi-GPU runs use RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("STF_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
     from stfunet import engine, nhwc
@@ -238,7 +246,7 @@ def main():
                         for k, d in kt.items()},
             "last_loss": round(last_loss, 5),
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)
     if world > 1:

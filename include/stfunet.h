@@ -160,17 +160,23 @@ int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const v
                       const float* scale, const float* shift, const float* mean,
                       const float* invstd, int mask_mode, const void* mask_src,
                       int mask_cstride, void* g_out, float* partial, stf_stream_t stream);
+/* (g_out may be NULL without dpool: the masked gradient is then not stored and
+ * stf_bn_bwd_apply recomputes the mask.) */
 /* dgamma, dbeta (summed over groups) and coef [groups][3][C] of dy = A*g + B*y + C. */
 int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C, int64_t M,
                         const float* gamma, const float* mean, const float* invstd,
                         float* dgamma, float* dbeta, float* coef, stf_stream_t stream);
-/* dy = A*g + B*y + C (bf16, dy_cstride; may alias g when dense); optional
- * per-tile column sums of dy for the bias of the producing conv
- * (bias_partial [stf_bn_bwd_apply_tiles][C]) reduced into dbias. */
+/* dy = A*g' + B*y + C (bf16, dy_cstride; may alias g when dense).  g' = g, or
+ * with mask_scale/mask_shift ([groups][C], the forward BN affine) the ReLU mask
+ * recomputed from y: g' = g where y*scale+shift > 0 else 0 -- then g is the raw
+ * incoming gradient (any channel stride) and stf_bn_bwd_reduce ran with
+ * g_out = NULL.  Optional per-tile column sums of dy for the bias of the
+ * producing conv (bias_partial [stf_bn_bwd_apply_tiles][C]) reduced into dbias. */
 int stf_bn_bwd_apply_tiles(int64_t M, int C);
-int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int64_t M, int C,
-                     int groups, const float* coef, void* dy, int dy_cstride,
-                     float* bias_partial, float* dbias, stf_stream_t stream);
+int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int y_cstride, int64_t M,
+                     int C, int groups, const float* mask_scale, const float* mask_shift,
+                     const float* coef, void* dy, int dy_cstride, float* bias_partial,
+                     float* dbias, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- head + loss
  * UNet OutConv fused with the last BN+ReLU (src/unet.py:16-17,37,56):

@@ -209,7 +209,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
         sg[j] += gj;
         sgx[j] += gj * (v[j] - mu[j]) * is[j];
       }
-      *reinterpret_cast<uint4*>(g_out + pix * C + cg * 8) = pack8(d);
+      if (g_out) *reinterpret_cast<uint4*>(g_out + pix * C + cg * 8) = pack8(d);
     } else {
       const int Wp = W / 2, Hp = H / 2;
       const long n = pix / ((long)Hp * Wp);
@@ -316,8 +316,11 @@ __global__ void bn_bwd_groupsum_kernel(const float* __restrict__ partial, int T,
   if (dbeta) dbeta[c] = (float)db;
 }
 
-__global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restrict__ y, int ycs, long M, int C,
-                                    long Mg, const float* __restrict__ coef, uint16_t* dy, int dycs,
+// dy = A*g' + B*y + C, g' = g (already masked) or, with mscale != NULL, the ReLU
+// mask recomputed from y: g' = (y*mscale+mshift > 0) ? g : 0 (saves the masked copy)
+__global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* __restrict__ y, int ycs, long M,
+                                    int C, long Mg, const float* __restrict__ coef, const float* __restrict__ mscale,
+                                    const float* __restrict__ mshift, uint16_t* dy, int dycs,
                                     float* __restrict__ bias_partial) {
   __shared__ float red[NT][9];
   const int CG = C / 8;
@@ -326,7 +329,7 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restric
   const int cg = (int)(gt % CG);
   float sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int cur_g = -1;
-  float A[8], B[8], Cc[8];
+  float A[8], B[8], Cc[8], ms[8], mh[8];
   for (long u = gt; u < units; u += (long)gridDim.x * NT) {
     const long pix = u / CG;
     const int grp = (int)(pix / Mg);
@@ -335,12 +338,20 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, const uint16_t* __restric
       load_affine(coef + (size_t)grp * 3 * C, cg * 8, A);
       load_affine(coef + (size_t)grp * 3 * C + C, cg * 8, B);
       load_affine(coef + (size_t)grp * 3 * C + 2 * C, cg * 8, Cc);
+      if (mscale) {
+        load_affine(mscale + (size_t)grp * C, cg * 8, ms);
+        load_affine(mshift + (size_t)grp * C, cg * 8, mh);
+      }
     }
     float gv[8], yv[8];
-    unpack8(*reinterpret_cast<const uint4*>(g + pix * C + cg * 8), gv);
+    unpack8(*reinterpret_cast<const uint4*>(g + pix * gcs + cg * 8), gv);
     unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), yv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { gv[j] = A[j] * gv[j] + B[j] * yv[j] + Cc[j]; sb[j] += gv[j]; }
+    for (int j = 0; j < 8; ++j) {
+      const float gj = (mscale && !(yv[j] * ms[j] + mh[j] > 0.f)) ? 0.f : gv[j];
+      gv[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+      sb[j] += gv[j];
+    }
     *reinterpret_cast<uint4*>(dy + pix * dycs + cg * 8) = pack8(gv);
   }
   if (!bias_partial) return;
@@ -428,6 +439,7 @@ extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpo
                                  int mask_cstride, void* g_out, float* partial, stf_stream_t stream) {
   if (!cg_ok(C) || y_cstride % 8 || (dz && dz_cstride % 8) || groups < 1 || N % groups) return STF_EINVAL;
   if (!dz && !dpool) return STF_EINVAL;
+  if (!g_out && dpool) return STF_EINVAL;            // the pooled routing must be materialized
   if (dpool && (((H | W) & 1) || mask_mode == 2)) return STF_EINVAL;
   if (mask_mode == 2 && (!mask_src || mask_cstride % 8)) return STF_EINVAL;
   const int tpg = stf_bn_bwd_tiles(N, H, W, C, groups, dpool != nullptr);
@@ -469,14 +481,16 @@ extern "C" int stf_bn_bwd_apply_tiles(int64_t M, int C) {
   return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
 }
 
-extern "C" int stf_bn_bwd_apply(const void* g, const void* y, int y_cstride, int64_t M, int C, int groups,
-                                const float* coef, void* dy, int dy_cstride, float* bias_partial, float* dbias,
-                                stf_stream_t stream) {
-  if (!cg_ok(C) || y_cstride % 8 || dy_cstride % 8 || groups < 1 || M % groups) return STF_EINVAL;
+extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int y_cstride, int64_t M, int C,
+                                int groups, const float* mask_scale, const float* mask_shift, const float* coef,
+                                void* dy, int dy_cstride, float* bias_partial, float* dbias, stf_stream_t stream) {
+  if (!cg_ok(C) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8 || groups < 1 || M % groups) return STF_EINVAL;
+  if ((mask_scale == nullptr) != (mask_shift == nullptr)) return STF_EINVAL;
   const int tiles = stf_bn_bwd_apply_tiles(M, C);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, (const uint16_t*)y,
-                     y_cstride, (long)M, C, (long)(M / groups), coef, (uint16_t*)dy, dy_cstride, bias_partial);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                     (const uint16_t*)y, y_cstride, (long)M, C, (long)(M / groups), coef, mask_scale, mask_shift,
+                     (uint16_t*)dy, dy_cstride, bias_partial);
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
     const int S = stf::colsum_stage1(bias_partial, tiles, C, s, 1, stf::FOLD16_ROWS);

@@ -557,20 +557,24 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
 // row offset (a tap shift moves the 16 rows a fragment reads by 0..2 rows).
 STF_DEV int swzh(int row, int kc) { return kc ^ ((row >> 1) & 2); }
 
-template <int PH, int PW, int DIAG>
-__global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
-                                                            int rem) {
-  constexpr int NW = 8, BN = 64, RPI = 16;              // 64-B rows: 16 per 1-KiB DMA instruction
+// NW waves x 64 pixels = PH x PW tile; STAGES = 2: one 8-wave workgroup per CU
+// with a 2-stage ring; STAGES = 1: two 4-wave workgroups per CU, single stage
+// each, so one workgroup's DMA wait and epilogue overlap the other's MFMAs.
+template <int PH, int PW, int NW, int STAGES, int DIAG>
+__global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes,
+                                                                                    int TY, int TX, int per, int rem) {
+  constexpr int NTH = 64 * NW, BN = 64, RPI = 16;       // 64-B rows: 16 per 1-KiB DMA instruction
   constexpr int HW = PW + 2, HR = (PH + 2) * HW;        // halo rows
   constexpr int HI = (HR + RPI * NW - 1) / (RPI * NW);  // halo DMA instructions per wave
   constexpr int WI = (9 * BN + RPI * NW - 1) / (RPI * NW);
   constexpr int HROWS = HI * RPI * NW, WROWS = WI * RPI * NW;
   constexpr int STAGE = (HROWS + WROWS) * 64;
   constexpr int PX = PH * PW, WTM = PX / NW, TM = WTM / 16, TN = BN / 16;
-  static_assert(PX % (16 * NW) == 0 && PW % 16 == 0 && PX == 512, "tile (epilogue: 8 stores per lane)");
+  constexpr int PPP = NTH / 8, NSTORE = PX / PPP;      // epilogue: pixels per pass, stores per lane
+  static_assert(WTM == 64 && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE, "epilogue scratch");
-  static_assert(2 * STAGE <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
@@ -631,7 +635,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(it0, 0, 0, true);
+  if (STAGES == 2) issue(it0, 0, 0, true);
   int iit = it0, icc = 0;                               // issue cursor (last issued stage)
   int cit = it0, ccc = 0;                               // compute cursor
   // BN partial statistics, one row per (group, workgroup): stats [groups][gridDim][2][Nout].
@@ -652,27 +656,39 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
   }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
   for (int s = 0; s < S; ++s) {
-    // retire this stage's DMA; the previous epilogue's 8 buffer stores (issued
-    // after it, stores and loads retire in order) may stay in flight
-    if (epi) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    epi = false;
-    __builtin_amdgcn_s_barrier();
-    // bias of this lane's 16 accumulator channels, loaded BEFORE the next DMA so
-    // that waiting for it never waits for the DMA
+    const int buf = STAGES == 2 ? (s & 1) : 0;
     f32x4 bv[TN];
-    if (ccc == CC - 1) {
-      const int nt = cit / ntiles;
+    auto load_bias = [&]() {
+      // bias of this lane's 16 accumulator channels, loaded BEFORE the next DMA so
+      // that waiting for it never waits for the DMA
+      if (ccc == CC - 1) {
+        const int nt = cit / ntiles;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bv[j] = __builtin_amdgcn_raw_buffer_load_b128(rs_bias, (nt * BN + j * 16 + fk * 4) * 4, 0, 0);
-    }
-    {
+        for (int j = 0; j < TN; ++j)
+          bv[j] = __builtin_amdgcn_raw_buffer_load_b128(rs_bias, (nt * BN + j * 16 + fk * 4) * 4, 0, 0);
+      }
+    };
+    if constexpr (STAGES == 2) {
+      // retire this stage's DMA; the previous epilogue's NSTORE buffer stores
+      // (issued after it, stores and loads retire in order) may stay in flight
+      if (epi) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      epi = false;
+      __builtin_amdgcn_s_barrier();
+      load_bias();
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
       issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
+    } else {
+      // single stage: every wave is done with the buffer, refill it, wait
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      load_bias();
+      issue(cit, ccc, 0, DIAG != 2 || s < 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
-    const char* hb = smem + (s & 1) * STAGE;
+    const char* hb = smem + buf * STAGE;
     if (DIAG == 3) { if (++ccc == CC) { ccc = 0; ++cit; } continue; }
     const char* wb = hb + HROWS * 64;
 #pragma unroll
@@ -699,12 +715,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
       // ---- epilogue through LDS: the stage just read becomes the output tile
       // [PX][64] bf16 (128-B rows, 16-B chunk c at c ^ (p & 7)); full-row 16-B
       // buffer stores (invalid pixels get an out-of-range offset, so every lane
-      // issues exactly 8 stores and the next stage can wait with vmcnt(8));
+      // issues exactly NSTORE stores and the next stage can wait with vmcnt(NSTORE));
       // BN partial sums from the stored values; raw barriers only, so nothing
       // drains the stores or the DMA already in flight.
       const int nt = cit / ntiles, tile = cit - nt * ntiles;
       const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
-      char* ot = smem + (s & 1) * STAGE;
+      char* ot = smem + buf * STAGE;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                     // every wave is done reading this stage
 #pragma unroll
@@ -728,8 +744,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
 #pragma unroll
-      for (int k = 0; k < PX / 64; ++k) {
-        const int p = (tid >> 3) + 64 * k;
+      for (int k = 0; k < NSTORE; ++k) {
+        const int p = (tid >> 3) + PPP * k;
         const int y = ty * PH + p / PW, x = tx * PW + p % PW;
         const bool ok = y < a.Hd && x < a.Wd;
         const int m = (img * a.Hd + y) * a.Wd + x;
@@ -792,7 +808,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(Geo a, uint32_t sr
   if (a.stats && tid < 128 && run_key >= 0) flush();
 }
 
-constexpr int HALO_PH = 16, HALO_PW = 32;
+constexpr int HALO_PW = 32;
+// variant: 0 = 16x32 tile, 8 waves, 2-stage ring (1 WG/CU); 1 = 8x32, 4 waves, 1 stage (2 WG/CU)
+int halo_variant() {
+  static const int v = [] { const char* e = getenv("STF_HALO_VARIANT"); return e ? atoi(e) : 0; }();
+  return v;
+}
+int halo_ph() { return halo_variant() == 1 ? 8 : 16; }
 
 int num_cus() {
   static const int n = [] {
@@ -920,7 +942,7 @@ int pick_mtile(const stf_igemm_args* a) {
 }
 
 void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
-  ty = (c.Hd + HALO_PH - 1) / HALO_PH;
+  ty = (c.Hd + halo_ph() - 1) / halo_ph();
   tx = (c.Wd + HALO_PW - 1) / HALO_PW;
 }
 
@@ -929,7 +951,7 @@ int halo_grid(const stf_igemm_args* a) {
   int ty, tx;
   halo_tiles(a->g, ty, tx);
   const long items = (long)a->g.N * ty * tx * (a->Nout / 64);
-  return (int)std::min<long>(items, num_cus());
+  return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 ? 2 : 1));
 }
 
 // BatchNorm partial-statistics rows per group for the kernel that will run
@@ -955,7 +977,10 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* tr = c.transposed ? "true" : "false";
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
-    case 'H': snprintf(buf, sizeof buf, "conv3x3_halo_kernel<%d, %d, 0>", HALO_PH, HALO_PW); break;
+    case 'H':
+      if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0>", HALO_PW);
+      else snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0>", HALO_PW);
+      break;
     case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d>", tr, sc, epi); break;
     case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d>", tr, sc, epi); break;
     case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, 0>", sc); break;
@@ -1006,9 +1031,15 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
     const long items = (long)c.N * ty * tx * (a->Nout / 64);
     const int grid = halo_grid(a);
     static const int diag = [] { const char* e = getenv("STF_HALO_DIAG"); return e ? atoi(e) : 0; }();
-#define STF_H(D) hipLaunchKernelGGL((conv3x3_halo_kernel<HALO_PH, HALO_PW, D>), dim3(grid), dim3(512), 0, s, g, \
-                                    src_bytes, ty, tx, (int)(items / grid), (int)(items % grid))
-    if (diag == 1) STF_H(1); else if (diag == 2) STF_H(2); else if (diag == 3) STF_H(3); else STF_H(0);
+#define STF_H(D) do {                                                                                            \
+    if (halo_variant() == 1)                                                                                     \
+      hipLaunchKernelGGL((conv3x3_halo_kernel<8, HALO_PW, 4, 1, D>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, \
+                         tx, (int)(items / grid), (int)(items % grid));                                          \
+    else                                                                                                         \
+      hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, src_bytes,   \
+                         ty, tx, (int)(items / grid), (int)(items % grid));                                      \
+  } while (0)
+    if (diag == 2) STF_H(2); else STF_H(0);
 #undef STF_H
     STF_CHECK_LAUNCH();
     return 0;

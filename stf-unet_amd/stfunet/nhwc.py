@@ -285,7 +285,6 @@ def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool:
     G = st.groups
     tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, G, int(dpool is not None))
     part = torch.empty(G * tiles * 2 * C, dtype=torch.float32, device=dev)
-    g = new_feat(y.N, y.H, y.W, C, dev)
     if dz is not None:
         dz.check()
         assert (dz.N, dz.H, dz.W, dz.C) == (y.N, y.H, y.W, C)
@@ -295,18 +294,30 @@ def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool:
     mode = 2 if mask is not None else (1 if relu else 0)
     if mask is not None:
         mask.check()
+    # without pooling / saved mask / a caller that needs it, the masked gradient is
+    # never stored: the apply pass re-reads dz and recomputes the ReLU mask from y
+    direct = dpool is None and mode != 2 and not keep_g
+    g = None if direct else new_feat(y.N, y.H, y.W, C, dev)
     call("stf_bn_bwd_reduce", dz.ptr() if dz is not None else None, dz.cs if dz is not None else 0,
          dpool.ptr() if dpool is not None else None, y.ptr(), y.cs, y.N, y.H, y.W, C, G, _p(st.scale),
          _p(st.shift), _p(st.mean), _p(st.invstd), mode, mask.ptr() if mask is not None else None,
-         mask.cs if mask is not None else 0, g.ptr(), _p(part), stream())
+         mask.cs if mask is not None else 0, g.ptr() if g is not None else None, _p(part), stream())
     if keep_g and out is None:
         out = new_feat(y.N, y.H, y.W, C, dev)
-    dy = bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=out)
+    if direct:
+        if out is None:
+            out = new_feat(y.N, y.H, y.W, C, dev)
+        dy = bn_backward_from_partial(dz, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=out,
+                                      mask_relu=(mode == 1))
+    else:
+        dy = bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=out)
     return (dy, g) if keep_g else dy
 
 
 def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None,
-                             out: Feat = None):
+                             out: Feat = None, mask_relu=False):
+    """Finalize + apply.  ``mask_relu``: g is the raw incoming gradient and the
+    ReLU mask is recomputed from y with the forward affine (g is not written)."""
     C = y.C
     dev = y.buf.device
     G = st.groups
@@ -320,6 +331,8 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
     if out is not None:
         out.check()
         assert (out.N, out.H, out.W, out.C) == (y.N, y.H, y.W, C)
-    call("stf_bn_bwd_apply", g.ptr(), y.ptr(), y.cs, y.M, C, G, _p(coef), dst.ptr(), dst.cs, _p(bpart),
-         _p(dbias), stream())
+    if mask_relu:
+        assert out is not None
+    call("stf_bn_bwd_apply", g.ptr(), g.cs, y.ptr(), y.cs, y.M, C, G, _p(st.scale) if mask_relu else None,
+         _p(st.shift) if mask_relu else None, _p(coef), dst.ptr(), dst.cs, _p(bpart), _p(dbias), stream())
     return dst
