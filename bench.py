@@ -68,24 +68,25 @@ def pmc_traffic(kernel, workload, batch):
     return (k["hbm_bytes_per_launch"], os.path.relpath(path, HERE)) if k else (None, None)
 
 
-def roofline(kt, workload, batch):
-    """Roofline of the dominant kernel (largest summed time in the timed region,
-    HIP events on its launch stream): algorithmic FLOPs per launch (2*M*N*K) over
-    its average launch duration, against the dense bf16 MFMA peak."""
+def roofline(kt, workload, batch, census):
+    """Roofline of the dominant kernel (largest summed time in the census step;
+    its every launch in the timed region bracketed by HIP events on its launch
+    stream): algorithmic FLOPs per launch (2*M*N*K) over its average launch
+    duration, against the dense bf16 MFMA peak."""
     if not kt:
         return None
     name = max(kt, key=lambda k: kt[k]["ms"])
     k = kt[name]
     traffic, src = pmc_traffic(name, workload, batch)
-    gemm_ms = sum(v["ms"] for v in kt.values())
-    gemm_fl = sum(v["flops"] for v in kt.values())
+    gemm_ms = sum(v["ms"] for v in census.values())
+    gemm_fl = sum(v["flops"] for v in census.values())
     return {"bound": "mfma", "kernel": name, "achieved": round(k["tflops"], 2), "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC 2*FETCH_SIZE+WRITE_SIZE)",
             "traffic_source": src, "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
             "algorithmic_tflop_per_launch": round(k["flops"] / k["launches"] / 1e12, 6),
-            "all_conv_gemm_kernels": {"ms": round(gemm_ms, 3),
-                                      "tflops": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else 0.0}}
+            "all_conv_gemm_kernels_census_step": {
+                "ms": round(gemm_ms, 3), "tflops": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else 0.0}}
 
 
 def cpu_baseline(args):
@@ -190,13 +191,23 @@ def main():
         sched.step()
         return loss
 
+    # warmup; its last step is a census (every conv-GEMM launch timed) that picks
+    # the dominant kernel, and only that kernel is instrumented in the timed
+    # region (per-launch events on every kernel perturb a host-bound step)
+    census = {}
     for i in range(args.warmup):
+        if i == args.warmup - 1 and not args.no_kernel_timer:
+            nhwc.TIMER = nhwc.KernelTimer()
         loss = train_step(i)
+        if nhwc.TIMER is not None:
+            census = nhwc.TIMER.summary()
+            nhwc.TIMER = None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     if not args.no_kernel_timer:
-        nhwc.TIMER = nhwc.KernelTimer()
+        dominant = max(census, key=lambda k: census[k]["ms"]) if census else None
+        nhwc.TIMER = nhwc.KernelTimer(only=dominant)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -226,7 +237,7 @@ def main():
                     if args.model == "unet" else
                     f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
                     f"{args.size}x{args.size} train step")
-        roof = roofline(kt, workload, args.batch)
+        roof = roofline(kt, workload, args.batch, census)
         res = {
             "metric": "training samples/sec (256x256 DCE-MRI frames)",
             "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -242,8 +253,8 @@ def main():
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
             "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
             "roofline": roof,
-            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in d.items()}
-                        for k, d in kt.items()},
+            "kernels_census_step": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in d.items()}
+                                    for k, d in census.items()},
             "last_loss": round(last_loss, 5),
         }
         if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only

@@ -170,8 +170,8 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(WArgs a) {
 // which bounds it by HBM at C = 64).  MFMA k-slot -> pixel is permuted so the
 // eight rows a 32-lane half reads with ds_read_b64_tr_b16 are eight consecutive
 // pixels, i.e. eight consecutive LDS rows (160 B stride: disjoint bank octets).
-// Waves: 2 (n) x 2 (c); each holds 32 n x 32 c x 9 taps = 36 accumulators.
-template <int PW>
+// Waves: 1 (n) x 4 (c); each holds 64 n x 16 c x 9 taps = 36 accumulators.
+template <int PW, int DIAG = 0>
 __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles) {
   constexpr int PH = 64 / PW, HW = PW + 2, HR = (PH + 2) * HW;
   constexpr int SR = 64 + 16;                   // LDS row stride (elements), 160 B
@@ -181,7 +181,10 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   __shared__ __attribute__((aligned(16))) uint16_t smem[2][A_EL + B_EL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  // wave = 16-channel slice of x (TN = 1) x all 64 dy channels (TM = 4): the dy
+  // fragments serve all nine taps, so fewer LDS reads per MFMA than 2 x 2 waves
+  constexpr int TMW = 4, TNW = 1;
+  const int wn = wave;
   const int split = blockIdx.x;
   const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
   const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
@@ -224,13 +227,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
     }
   };
 
-  f32x4 acc[9][2][2];
+  f32x4 acc[9][TMW][TNW];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TMW; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TNW; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // lane (g, q, p4): k-slot 8g + 4h + q (h = lo/hi read) holds pixel
   // 16(g>>1) + 8h + 4(g&1) + q of the 32-pixel step.
@@ -251,15 +254,16 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   __syncthreads();
   for (int it = 0; it < steps; ++it) {
     const int cur = it & 1;
-    if (it + 1 < steps) load(t_begin + it + 1);
+    if (it + 1 < steps && (DIAG != 1 || it < 1)) load(t_begin + it + 1);
     const uint16_t* sa = smem[cur];
     const uint16_t* sb = sa + A_EL;
+    if (DIAG == 2) { if (it + 1 < steps) store(cur ^ 1); __syncthreads(); continue; }
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      bf16x8 af[2];
+      bf16x8 af[TMW];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wm * 32 + i * 16 + p4;
+      for (int i = 0; i < TMW; ++i) {
+        const int col = i * 16 + p4;
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][0] + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][1] + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -268,19 +272,19 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int toff = ((t / 3) * HW + t % 3) * SR;
-        bf16x8 bfr[2];
+        bf16x8 bfr[TNW];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = wn * 32 + j * 16 + p4;
+        for (int j = 0; j < TNW; ++j) {
+          const int col = wn * 16 * TNW + j * 16 + p4;
           v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][0] + toff + col));
           v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][1] + toff + col));
           short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           bfr[j] = __builtin_bit_cast(bf16x8, s8);
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TMW; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < TNW; ++j)
             acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
       }
     }
@@ -293,13 +297,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TMW; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int k = t * a.Cs + c0 + wn * 32 + j * 16 + (lane & 15);
+      for (int j = 0; j < TNW; ++j) {
+        const int k = t * a.Cs + c0 + wn * 16 * TNW + j * 16 + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int n = n0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
           out[(size_t)n * RSC + k] = acc[t][i][j][r];
         }
       }
@@ -396,7 +400,12 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
     dim3 grid(splits, a->Nout / 64, c.Cs / 64);
-    if (pw == 16)
+    static const int diag = [] { const char* e = getenv("STF_WGRAD_DIAG"); return e ? atoi(e) : 0; }();
+    if (pw == 16 && diag == 1)
+      hipLaunchKernelGGL((wgrad3x3_kernel<16, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (pw == 16 && diag == 2)
+      hipLaunchKernelGGL((wgrad3x3_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (pw == 16)
       hipLaunchKernelGGL((wgrad3x3_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else
       hipLaunchKernelGGL((wgrad3x3_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt);

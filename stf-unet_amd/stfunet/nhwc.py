@@ -25,10 +25,15 @@ def _p(t):
 
 class KernelTimer:
     """Brackets kernel launches with HIP events on the launching stream and
-    accumulates algorithmic FLOPs per kernel family (bench.py's roofline)."""
+    accumulates algorithmic FLOPs per device kernel (bench.py's roofline).
+    ``only``: instrument just this kernel name (the others cost nothing)."""
 
-    def __init__(self):
+    def __init__(self, only=None):
         self.rec = {}
+        self.only = only
+
+    def wants(self, name):
+        return self.only is None or name == self.only
 
     def begin(self):
         ev = torch.cuda.Event(enable_timing=True)
@@ -52,6 +57,14 @@ class KernelTimer:
 
 
 TIMER = None   # set to a KernelTimer to instrument igemm / wgrad launches
+_NAMES = {}    # launch signature -> device kernel name (stf_*_kernel_name)
+
+
+def _kernel_name(fn, key, args):
+    n = _NAMES.get(key)
+    if n is None:
+        n = _NAMES[key] = getattr(_lib.load(), fn)(ctypes.byref(args)).decode()
+    return n
 
 
 @dataclass
@@ -147,11 +160,15 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
         a.stats = _p(stats)
     t = TIMER
+    if t is not None:
+        name = _kernel_name("stf_igemm_kernel_name", ("i", src.N, src.H, src.W, src.C, Hd, Wd, nout, R, S, stride,
+                                                      pad, transposed, scatter2x2, lstm is not None, groups), a)
+        if not t.wants(name):
+            t = None
     ev = t.begin() if t is not None else None
     call("stf_igemm", ctypes.byref(a), stream())
     if t is not None:
         macs = src.N * Hd * Wd * nout * R * S * src.C
-        name = _lib.load().stf_igemm_kernel_name(ctypes.byref(a)).decode()
         t.end(ev, name, 2.0 * macs / (stride * stride if transposed else 1))
     return stats, tiles
 
@@ -185,10 +202,14 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
     a.ws = _p(ws)
     a.splits = splits.value
     t = TIMER
+    if t is not None:
+        name = _kernel_name("stf_wgrad_kernel_name", ("w", x.N, x.H, x.W, x.C, dy.H, dy.W, dy.C, R, S, stride, pad), a)
+        if not t.wants(name):
+            t = None
     ev = t.begin() if t is not None else None
     call("stf_wgrad", ctypes.byref(a), stream())
     if t is not None:
-        t.end(ev, _lib.load().stf_wgrad_kernel_name(ctypes.byref(a)).decode(), 2.0 * dy.M * dy.C * R * S * x.C)
+        t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad_reduce", _p(ws), splits.value, dy.C, R, S, x.C, _p(out), stream())
 
 
