@@ -231,6 +231,15 @@ int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* o
  *          forward gather with pad' = R-1-pad) */
 int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int mode, int cpad,
                     void* out, stf_stream_t stream);
+/* Many stf_pack_weight jobs in one launch.  descs: DEVICE array of count
+ * descriptors (same fields and modes as stf_pack_weight); max_elems = the
+ * largest packed element count among them (sizes the grid). */
+typedef struct stf_pack_desc {
+  const float* w;
+  void* out;
+  int d0, d1, R, S, mode, cpad;
+} stf_pack_desc;
+int stf_pack_weights(const stf_pack_desc* descs, int count, int64_t max_elems, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- STF-LSTM-UNet
  * x [B][Ttot][C][H][W] fp32 -> t-major NHWC bf16 [T*B][H][W][Cpad]: frame t of

@@ -62,49 +62,55 @@ __global__ void pack_input_kernel(const float* __restrict__ x, int N, int C, int
   }
 }
 
-// out element index -> source index, per mode (see include/stfunet.h)
+// out element index -> source value, per mode (see include/stfunet.h).  32-bit
+// index math (every packed weight is < 2^31 elements; stf_pack_weight(s) check).
+STF_DEV float pack_src(const float* __restrict__ w, int d0, int d1, int R, int S, int mode, int cpad, int o) {
+  const int RS = R * S;
+  if (mode == 0) {              // Conv2d w[Co=d0][Ci=d1][R][S] -> [Co][R][S][cpad]
+    const int t = o / cpad, c = o - t * cpad;
+    const int co = t / RS, tap = t - co * RS;
+    return c < d1 ? w[(co * d1 + c) * RS + tap] : 0.f;
+  } else if (mode == 1) {       // Conv2d -> [Ci][R][S][Co]
+    const int t = o / d0, co = o - t * d0;
+    const int ci = t / RS, tap = t - ci * RS;
+    return w[(co * d1 + ci) * RS + tap];
+  } else if (mode == 2) {       // ConvT w[Ci=d0][Co=d1][R][S] -> [(tap)*Co + co][Ci]
+    const int t = o / d0, ci = o - t * d0;
+    const int tap = t / d1, co = t - tap * d1;
+    return w[(ci * d1 + co) * RS + tap];
+  } else if (mode == 3) {       // ConvT -> [Ci][R][S][Co]
+    const int t = o / d1, co = o - t * d1;
+    const int ci = t / RS, tap = t - ci * RS;
+    return w[(ci * d1 + co) * RS + tap];
+  } else if (mode == 5) {       // Conv2d -> [Ci][R-1-r][S-1-s][Co] (stride-1 dgrad as a forward gather)
+    const int t = o / d0, co = o - t * d0;
+    const int ci = t / RS, tap = t - ci * RS;
+    const int r = tap / S, s_ = tap - r * S;
+    return w[(co * d1 + ci) * RS + (R - 1 - r) * S + (S - 1 - s_)];
+  }
+  // mode 4: ConvT -> [Co][R][S][Ci]
+  const int t = o / d0, ci = o - t * d0;
+  const int co = t / RS, tap = t - co * RS;
+  return w[(ci * d1 + co) * RS + tap];
+}
+
+STF_DEV long pack_total(int d0, int d1, int R, int S, int mode, int cpad) {
+  return mode == 0 ? (long)d0 * R * S * cpad : (long)d0 * d1 * R * S;
+}
+
 __global__ void pack_weight_kernel(const float* __restrict__ w, int d0, int d1, int R, int S, int mode, int cpad,
                                    uint16_t* __restrict__ out) {
-  const int RS = R * S;
-  long total;
-  if (mode == 0) total = (long)d0 * RS * cpad;
-  else total = (long)d0 * d1 * RS;
-  for (long o = blockIdx.x * (long)NT + threadIdx.x; o < total; o += (long)gridDim.x * NT) {
-    float v = 0.f;
-    if (mode == 0) {            // Conv2d w[Co=d0][Ci=d1][R][S] -> [Co][R][S][cpad]
-      const int c = (int)(o % cpad);
-      const long t = o / cpad;
-      const int tap = (int)(t % RS), co = (int)(t / RS);
-      if (c < d1) v = w[((long)co * d1 + c) * RS + tap];
-    } else if (mode == 1) {     // Conv2d -> [Ci][R][S][Co]
-      const int co = (int)(o % d0);
-      const long t = o / d0;
-      const int tap = (int)(t % RS), ci = (int)(t / RS);
-      v = w[((long)co * d1 + ci) * RS + tap];
-    } else if (mode == 2) {     // ConvT w[Ci=d0][Co=d1][R][S] -> [(tap)*Co + co][Ci]
-      const int ci = (int)(o % d0);
-      const long t = o / d0;
-      const int co = (int)(t % d1), tap = (int)(t / d1);
-      v = w[((long)ci * d1 + co) * RS + tap];
-    } else if (mode == 3) {     // ConvT -> [Ci][R][S][Co]
-      const int co = (int)(o % d1);
-      const long t = o / d1;
-      const int tap = (int)(t % RS), ci = (int)(t / RS);
-      v = w[((long)ci * d1 + co) * RS + tap];
-    } else if (mode == 5) {     // Conv2d -> [Ci][R-1-r][S-1-s][Co] (stride-1 dgrad as a forward gather)
-      const int co = (int)(o % d0);
-      const long t = o / d0;
-      const int tap = (int)(t % RS), ci = (int)(t / RS);
-      const int r = tap / S, s_ = tap - r * S;
-      v = w[((long)co * d1 + ci) * RS + (R - 1 - r) * S + (S - 1 - s_)];
-    } else {                    // mode 4: ConvT -> [Co][R][S][Ci]
-      const int ci = (int)(o % d0);
-      const long t = o / d0;
-      const int tap = (int)(t % RS), co = (int)(t / RS);
-      v = w[((long)ci * d1 + co) * RS + tap];
-    }
-    reinterpret_cast<bf16*>(out)[o] = f2bf(v);
-  }
+  const int total = (int)pack_total(d0, d1, R, S, mode, cpad);
+  for (int o = blockIdx.x * NT + threadIdx.x; o < total; o += gridDim.x * NT)
+    reinterpret_cast<bf16*>(out)[o] = f2bf(pack_src(w, d0, d1, R, S, mode, cpad, o));
+}
+
+// every descriptor of the list in one launch: blockIdx.y = descriptor
+__global__ void pack_weights_kernel(const stf_pack_desc* __restrict__ descs) {
+  const stf_pack_desc d = descs[blockIdx.y];
+  const int total = (int)pack_total(d.d0, d.d1, d.R, d.S, d.mode, d.cpad);
+  for (int o = blockIdx.x * NT + threadIdx.x; o < total; o += gridDim.x * NT)
+    reinterpret_cast<bf16*>(d.out)[o] = f2bf(pack_src(d.w, d.d0, d.d1, d.R, d.S, d.mode, d.cpad, o));
 }
 
 __global__ void channel_sum_kernel(const uint16_t* __restrict__ x, int xcs, long M, int C,
@@ -162,8 +168,18 @@ extern "C" int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int
                                stf_stream_t stream) {
   if (mode < 0 || mode > 5 || (mode == 0 && cpad < d1)) return STF_EINVAL;
   const long total = mode == 0 ? (long)d0 * R * S * cpad : (long)d0 * d1 * R * S;
+  if (total >= (1L << 31) || (long)d0 * d1 * R * S >= (1L << 31)) return STF_EINVAL;
   hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total, 4096)), dim3(NT), 0, (hipStream_t)stream, w, d0, d1,
                      R, S, mode, cpad, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_pack_weights(const stf_pack_desc* descs, int count, int64_t max_elems, stf_stream_t stream) {
+  if (count <= 0) return 0;
+  if (count > 65535 || max_elems <= 0 || max_elems >= (1L << 31)) return STF_EINVAL;
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(grid_for(max_elems, 1024), count), dim3(NT), 0, (hipStream_t)stream,
+                     descs);
   STF_CHECK_LAUNCH();
   return 0;
 }

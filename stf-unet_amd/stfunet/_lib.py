@@ -67,6 +67,7 @@ _SIGS = {
                           P]),
     "stf_pack_input": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_pack_weights": (c_int, [P, c_int, c_int64, P]),
     "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_maxpool3s2_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),

@@ -119,8 +119,82 @@ def pack_input(x, cpad):
     return f
 
 
+class _PackDesc(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("d0", ctypes.c_int), ("d1", ctypes.c_int),
+                ("R", ctypes.c_int), ("S", ctypes.c_int), ("mode", ctypes.c_int), ("cpad", ctypes.c_int)]
+
+
+class PackCache:
+    """Persistent bf16 GEMM packings of one model's fp32 master weights.
+
+    The first step packs on demand and records every (weight, layout) request;
+    from then on ``refresh()`` (called at the start of each forward, after the
+    optimizer step) repacks the whole recorded list with ONE stf_pack_weights
+    launch and ``get()`` returns the cached buffers.  Only the owning program
+    uses it (``ACTIVE_PACKS`` while its forward/backward runs), and the keys are
+    that model's parameters, so a cached packing is never stale."""
+
+    def __init__(self):
+        self.bufs = {}
+        self.seen = {}
+        self.recorded = ()
+        self.fresh = set()
+        self._desc = None
+
+    def refresh(self):
+        if self.seen:
+            self.recorded = tuple(self.seen)
+        self.seen = {}
+        self.fresh = set()
+        if not self.recorded:
+            return
+        if self._desc is None or self._desc[0] != self.recorded:
+            arr = (_PackDesc * len(self.recorded))()
+            mx = 0
+            for i, key in enumerate(self.recorded):
+                w, buf, mode, cpad = self.bufs[key]
+                d0, d1, R, S = w.shape
+                arr[i] = _PackDesc(w.data_ptr(), buf.data_ptr(), d0, d1, R, S, mode, cpad)
+                mx = max(mx, buf.numel())
+            dev = self.bufs[self.recorded[0]][1].device
+            t = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+            self._desc = (self.recorded, t, mx)
+        _, t, mx = self._desc
+        call("stf_pack_weights", _p(t), len(self.recorded), mx, stream())
+        self.fresh = set(self.recorded)
+
+    def get(self, w, mode, cpad):
+        w = w.detach()
+        key = (w.data_ptr(), tuple(w.shape), mode, cpad)
+        self.seen[key] = None
+        ent = self.bufs.get(key)
+        if ent is None:
+            ent = self.bufs[key] = (w, _pack_into(w, mode, cpad, None, launch=False), mode, cpad)
+        if key not in self.fresh:
+            _pack_into(w, mode, cpad, ent[1])
+            self.fresh.add(key)
+        return ent[1]
+
+
+ACTIVE_PACKS = None    # the running program's PackCache (None: pack on every call)
+
+
+def _pack_into(w, mode, cpad, out, launch=True):
+    assert w.dtype == torch.float32 and w.is_contiguous()
+    d0, d1, R, S = w.shape
+    n = d0 * R * S * cpad if mode == 0 else d0 * d1 * R * S
+    if out is None:
+        out = torch.empty(n, dtype=BF16, device=w.device)
+    if launch:
+        call("stf_pack_weight", _p(w), d0, d1, R, S, mode, cpad, _p(out), stream())
+    return out
+
+
 def pack_weight(w, mode, cpad=0):
-    """fp32 master weight -> bf16 GEMM rows (modes: include/stfunet.h)."""
+    """fp32 master weight -> bf16 GEMM rows (modes: include/stfunet.h); served
+    from the active program's PackCache when one is running."""
+    if ACTIVE_PACKS is not None:
+        return ACTIVE_PACKS.get(w, mode, cpad)
     w = w.detach()
     assert w.dtype == torch.float32 and w.is_contiguous()
     d0, d1, R, S = w.shape

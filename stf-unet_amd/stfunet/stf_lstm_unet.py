@@ -229,6 +229,7 @@ class LSTMProgram:
 class STFProgram:
     def __init__(self, m):
         self.m = m
+        self.packs = nhwc.PackCache()
         self.flat = FlatParams(m)
         self.grad_ready_hook = None
         self.layers = []
@@ -255,6 +256,22 @@ class STFProgram:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
+        """Refresh the packed weights (one launch) and run the forward schedule."""
+        self.packs.refresh()
+        nhwc.ACTIVE_PACKS = self.packs
+        try:
+            return self._forward(x, training, need_bwd)
+        finally:
+            nhwc.ACTIVE_PACKS = None
+
+    def backward(self, S, dlogits):
+        nhwc.ACTIVE_PACKS = self.packs
+        try:
+            return self._backward(S, dlogits)
+        finally:
+            nhwc.ACTIVE_PACKS = None
+
+    def _forward(self, x, training, need_bwd):
         m = self.m
         nhwc._NBT_PENDING.clear()
         dev = x.device
@@ -363,7 +380,7 @@ class STFProgram:
         return logits, (S if need_bwd else None)
 
     # ------------------------------------------------------------------ backward
-    def backward(self, S, dlogits):
+    def _backward(self, S, dlogits):
         m = self.m
         gv = self.flat.grad_view
         dev = dlogits.device

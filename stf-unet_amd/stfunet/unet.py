@@ -103,6 +103,7 @@ class DoubleConvProgram:
 class UNetProgram:
     def __init__(self, model):
         self.m = model
+        self.packs = nhwc.PackCache()
         self.levels = [DoubleConvProgram(b) for b in (model.enc1, model.enc2, model.enc3, model.enc4)]
         self.bott = DoubleConvProgram(model.bottleneck)
         self.ups = [model.up4, model.up3, model.up2, model.up1]
@@ -120,6 +121,22 @@ class UNetProgram:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
+        """Refresh the packed weights (one launch) and run the forward schedule."""
+        self.packs.refresh()
+        nhwc.ACTIVE_PACKS = self.packs
+        try:
+            return self._forward(x, training, need_bwd)
+        finally:
+            nhwc.ACTIVE_PACKS = None
+
+    def backward(self, S, dlogits):
+        nhwc.ACTIVE_PACKS = self.packs
+        try:
+            return self._backward(S, dlogits)
+        finally:
+            nhwc.ACTIVE_PACKS = None
+
+    def _forward(self, x, training, need_bwd):
         m = self.m
         nhwc._NBT_PENDING.clear()
         N, _, H, W = x.shape
@@ -169,7 +186,7 @@ class UNetProgram:
         return logits, (S if need_bwd else None)
 
     # ------------------------------------------------------------------ backward
-    def backward(self, S, dlogits):
+    def _backward(self, S, dlogits):
         m = self.m
         gv = self.flat.grad_view
         dev = dlogits.device

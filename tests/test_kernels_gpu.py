@@ -323,3 +323,26 @@ def test_adamw_flat_matches_oracle():
     b1, b2 = 0.9, 0.999
     call("stf_adamw", _p(p0), _p(g), _p(m), _p(v), n, 1e-3, b1, b2, 1e-8, 1e-4, 1 - b1 ** 3, 1 - b2 ** 3, stream())
     assert rel(p0, pr) < 1e-6 and rel(m, mr) < 1e-6 and rel(v, vr) < 1e-6
+
+
+def test_pack_weights_batched_matches_single():
+    """stf_pack_weights (one launch, every layout) == stf_pack_weight per tensor, bit for bit."""
+    from stfunet import nhwc
+    jobs = [((64, 8, 3, 3), 0, 8), ((128, 64, 3, 3), 0, 64), ((64, 128, 3, 3), 5, 0), ((64, 32, 3, 3), 1, 0),
+            ((256, 128, 2, 2), 2, 0), ((256, 128, 2, 2), 3, 0), ((64, 32, 3, 3), 4, 0), ((96, 40, 1, 1), 0, 48)]
+    cache = nhwc.PackCache()
+    ws = [torch.randn(*shape, device=DEV) for shape, _, _ in jobs]
+    nhwc.ACTIVE_PACKS = cache
+    try:
+        first = [cache.get(w, mode, cpad).clone() for w, (_, mode, cpad) in zip(ws, jobs)]   # on-demand + record
+        for w in ws:
+            w.mul_(-0.5)                                         # "optimizer step"
+        cache.refresh()                                          # one batched launch
+        batched = [cache.get(w, mode, cpad) for w, (_, mode, cpad) in zip(ws, jobs)]
+    finally:
+        nhwc.ACTIVE_PACKS = None
+    assert len(cache.recorded) == len(jobs)
+    for w, (_, mode, cpad), b, f in zip(ws, jobs, batched, first):
+        single = nhwc.pack_weight(w, mode, cpad)
+        assert torch.equal(b, single)
+        assert not torch.equal(b, f)

@@ -8,7 +8,8 @@ sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "stf-
 import torch
 from stfunet import nhwc
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+B = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64
+STF = "--stf" in sys.argv
 R = 5
 dev = "cuda"
 
@@ -24,6 +25,34 @@ def timeit(fn):
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / R
 
+
+if STF:
+    # STF-LSTM-UNet encoder (T=8 x B=16 = 128 images): ResNet-34 layer convs + LSTM step GEMMs
+    imgs = 128
+    tot = {"fwd": [0, 0], "dgrad": [0, 0], "wgrad": [0, 0]}
+    for name, h, ci, co, st in (("l1", 64, 64, 64, 1), ("l2.s2", 64, 64, 128, 2), ("l2", 32, 128, 128, 1),
+                                ("l3.s2", 32, 128, 256, 2), ("l3", 16, 256, 256, 1), ("l4.s2", 16, 256, 512, 2),
+                                ("l4", 8, 512, 512, 1)):
+        ho = h // st
+        x = nhwc.new_feat(imgs, h, h, ci, dev)
+        x.buf.normal_()
+        y = nhwc.new_feat(imgs, ho, ho, co, dev)
+        y.buf.normal_()
+        w = torch.randn(co, ci, 3, 3, device=dev) * 0.05
+        wp = nhwc.pack_weight(w, 0, ci)
+        flops = 2.0 * imgs * ho * ho * co * 9 * ci
+        tf = timeit(lambda: nhwc.igemm(x, wp, co, y, 3, 3, st, 1, want_stats=True, groups=8))
+        td = timeit(lambda: nhwc.conv_dgrad(y, w, x, 3, 3, st, 1))
+        out = torch.empty(co * ci * 9, device=dev)
+        tw = timeit(lambda: nhwc.wgrad(y, x, 3, 3, st, 1, out))
+        for k, t in (("fwd", tf), ("dgrad", td), ("wgrad", tw)):
+            tot[k][0] += t
+            tot[k][1] += flops
+        print(f"{name:8s} {ho:4d}^2 {ci:5d}->{co:5d}  GF {flops/1e9:8.1f}  fwd {tf:7.3f} ms {flops/tf/1e9:7.1f} TF"
+              f"  dgrad {td:7.3f} ms {flops/td/1e9:7.1f} TF  wgrad {tw:7.3f} ms {flops/tw/1e9:7.1f} TF", flush=True)
+    for k, (t, f) in tot.items():
+        print(f"TOTAL {k}: {t:.2f} ms  {f/t/1e9:.1f} TF/s")
+    sys.exit(0)
 
 layers = []
 H = 256
