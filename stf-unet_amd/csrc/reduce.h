@@ -46,7 +46,7 @@ static inline int colsum_stage1(float* buf, long T, long W, hipStream_t st, int 
 // of base[t * stride + c] (fp64); fold16_finish returns the total (fixed order)
 // on lane 0.  Consumers (finalize kernels) read <= a few hundred rows this way
 // without a separate folding launch.
-STF_DEV double fold16_partial(const float* base, int S, long stride, int c, bool cok) {
+STF_DEV double fold16_partial(const float* base, int S, long stride, long c, bool cok) {
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;       // four chains: the loads pipeline
   if (cok) {
     int t = threadIdx.x >> 4;

@@ -309,17 +309,22 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Nout, int R, int S,
-                                    int Cs, float* __restrict__ out) {
+// One launch: block = 16 outputs x 16 split-lanes; lane r sums slabs r, r+16, ...
+// (4 chains), the 16 lane totals are added in fixed order and written in the
+// PyTorch [Nout][Cs][R][S] layout (deterministic, no folding pass).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Nout, int R,
+                                                           int S, int Cs, float* __restrict__ out) {
+  __shared__ double red[256];
   const int RSC = R * S * Cs;
-  const size_t total = (size_t)Nout * RSC;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(size_t)k * total + idx];
-    const int n = idx / RSC, rem = idx - (size_t)n * RSC;
+  const long total = (long)Nout * RSC;
+  const long idx = blockIdx.x * 16L + (threadIdx.x & 15);
+  const bool ok = idx < total;
+  const double v = stf::fold16_partial(ws, ok ? splits : 0, total, ok ? idx : 0, ok);
+  const double t = stf::fold16_finish(v, red);
+  if (ok && (threadIdx.x >> 4) == 0) {
+    const int n = (int)(idx / RSC), rem = (int)(idx - (long)n * RSC);
     const int tap = rem / Cs, c = rem - tap * Cs;
-    out[((size_t)n * Cs + c) * (R * S) + tap] = s;
+    out[((long)n * Cs + c) * (R * S) + tap] = (float)t;
   }
 }
 
@@ -425,11 +430,9 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
 
 extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs, float* out,
                                 stf_stream_t stream) {
-  const size_t total = (size_t)Nout * R * S * Cs;
-  const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-  const int rows = stf::colsum_stage1(ws, splits, (long)total, (hipStream_t)stream);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ws, rows, Nout,
-                     R, S, Cs, out);
+  const long total = (long)Nout * R * S * Cs;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, (hipStream_t)stream, ws,
+                     splits, Nout, R, S, Cs, out);
   STF_CHECK_LAUNCH();
   return 0;
 }
