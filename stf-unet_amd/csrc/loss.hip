@@ -36,39 +36,47 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
                                 const float* __restrict__ scale, const float* __restrict__ shift,
                                 const float* __restrict__ w, const float* __restrict__ bias,
                                 float* __restrict__ logits) {
+  // CG lanes of one pixel are adjacent (NT and the grid stride are multiples of
+  // CG, so a thread's channel group is fixed); 4 pixels per thread per round so
+  // four 16-B loads are in flight before any arithmetic
+  constexpr int U = 4;
   const int CG = C / 8;
   const long units = P * CG;
-  // CG lanes of one pixel are adjacent; loop bound is uniform per CG group
-  for (long u0 = blockIdx.x * (long)NT; u0 < units; u0 += (long)gridDim.x * NT) {
-    const long u = u0 + threadIdx.x;
-    const bool ok = u < units;
-    const int cg = (int)(u % CG);
-    const long pix = u / CG;
-    float acc[K];
+  const int cg = (int)((blockIdx.x * (long)NT + threadIdx.x) % CG);
+  float sc[8], sh[8], wk[K][8], bk[K];
+  load8f(scale + cg * 8, sc);
+  load8f(shift + cg * 8, sh);
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] = 0.f;
-    if (ok) {
-      float v[8], sc[8], sh[8];
-      unpack8(*reinterpret_cast<const uint4*>(y + pix * C + cg * 8), v);
-      load8f(scale + cg * 8, sc);
-      load8f(shift + cg * 8, sh);
+  for (int k = 0; k < K; ++k) { load8f(w + k * C + cg * 8, wk[k]); bk[k] = bias[k]; }
+  const long stride = (long)gridDim.x * NT;
+  for (long u0 = blockIdx.x * (long)NT; u0 < units; u0 += stride * U) {
+    uint4 raw[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j] * sc[j] + sh[j], 0.f);
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float wk[8];
-        load8f(w + k * C + cg * 8, wk);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[k] += v[j] * wk[j];
-      }
+    for (int r = 0; r < U; ++r) {
+      const long u = u0 + r * stride + threadIdx.x;
+      raw[r] = u < units ? *reinterpret_cast<const uint4*>(y + (u / CG) * C + cg * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      for (int o = 1; o < CG; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
-    if (ok && cg == 0) {
-      const long n = pix / HW, hw = pix - n * HW;
+    for (int r = 0; r < U; ++r) {
+      const long u = u0 + r * stride + threadIdx.x;
+      float v[8], acc[K];
+      unpack8(raw[r], v);
 #pragma unroll
-      for (int k = 0; k < K; ++k) logits[(n * K + k) * HW + hw] = acc[k] + bias[k];
+      for (int k = 0; k < K; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = fmaxf(v[j] * sc[j] + sh[j], 0.f);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] += a * wk[k][j];
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        for (int o = 1; o < CG; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+      if (u < units && cg == 0) {
+        const long pix = u / CG, n = pix / HW, hw = pix - n * HW;
+#pragma unroll
+        for (int k = 0; k < K; ++k) logits[(n * K + k) * HW + hw] = acc[k] + bk[k];
+      }
     }
   }
 }

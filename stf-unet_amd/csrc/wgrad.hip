@@ -309,6 +309,136 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       }
 }
 
+// ---------------------------------------------------------------------------
+// ConvTranspose2d(k=2, s=2) weight gradient: one block per (64 dy-channel,
+// 64 x-channel) tile covers all four taps.
+//   dW[n][tap][c] = sum_p dy[p][n] * x[(2py + r, 2px + s)][c],  p over the small grid
+// The taps read disjoint sub-pixels of x, staged as four sub-images of the pixel
+// tile (LDS row = tap * 64 + p), so both operands cross HBM once (the per-tap
+// kernel reads dy four times) and each tap's transposed reads hit consecutive
+// rows.  Single LDS buffer (51 KB) -> 3 blocks per CU; the next tile's global
+// loads are in flight (registers) during the MFMAs of the current one.
+template <int PW>
+__global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles) {
+  constexpr int PH = 64 / PW, SR = 64 + 16;
+  constexpr int A_EL = 64 * SR, B_EL = 4 * 64 * SR;
+  constexpr int CHA = 64 * 8 / NT, CHB = 4 * 64 * 8 / NT;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[A_EL + B_EL];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int TMW = 4;                        // all 64 dy channels per wave, 16 x channels (wave)
+  const int split = blockIdx.x;
+  const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
+  const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
+  const int per_img = tiles_y * tiles_x;
+
+  uint4 ra[CHA], rb[CHB];
+  auto load = [&](int t) {
+    const int img = t / per_img, rem = t - img * per_img;
+    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    const int y0 = ty * PH, x0 = tx * PW;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) {
+      const int e = tid + i * NT, px = e >> 3, ch = e & 7;
+      const int yd = y0 + px / PW, xd = x0 + px % PW;
+      ra[i] = make_uint4(0, 0, 0, 0);
+      if (yd < a.Hd && xd < a.Wd)
+        ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int e = tid + i * NT, row = e >> 3, ch = e & 7;
+      const int tap = row >> 6, p = row & 63;
+      const int yd = y0 + p / PW, xd = x0 + p % PW;
+      const int ys = 2 * yd + (tap >> 1), xs = 2 * xd + (tap & 1);
+      rb[i] = make_uint4(0, 0, 0, 0);
+      if (yd < a.Hd && xd < a.Wd)
+        rb[i] = *reinterpret_cast<const uint4*>(a.x + (size_t)((img * a.Hs + ys) * a.Ws + xs) * a.xcs + c0 + ch * 8);
+    }
+  };
+  auto store = [&]() {
+    uint16_t* sa = smem;
+    uint16_t* sb = smem + A_EL;
+#pragma unroll
+    for (int i = 0; i < CHA; ++i) {
+      const int e = tid + i * NT;
+      *reinterpret_cast<uint4*>(sa + (e >> 3) * SR + (e & 7) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CHB; ++i) {
+      const int e = tid + i * NT;
+      *reinterpret_cast<uint4*>(sb + (e >> 3) * SR + (e & 7) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][TMW];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < TMW; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry and pixel permutation as in wgrad3x3_kernel
+  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
+  const int pl = 16 * (g >> 1) + 4 * (g & 1) + q;
+  int prow[2][2];
+#pragma unroll
+  for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) prow[k2][h] = (32 * k2 + 8 * h + pl) * SR;
+
+  const int steps = t_end - t_begin;
+  if (steps > 0) { load(t_begin); store(); }
+  __syncthreads();
+  for (int it = 0; it < steps; ++it) {
+    if (it + 1 < steps) load(t_begin + it + 1);
+    const uint16_t* sa = smem;
+    const uint16_t* sb = smem + A_EL;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 af[TMW];
+#pragma unroll
+      for (int i = 0; i < TMW; ++i) {
+        const int col = i * 16 + p4;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][0] + col));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][1] + col));
+        short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, s8);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int col = wave * 16 + p4;
+        const int toff = t * 64 * SR;
+        v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + toff + prow[k2][0] + col));
+        v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + toff + prow[k2][1] + col));
+        short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, s8);
+#pragma unroll
+        for (int i = 0; i < TMW; ++i)
+          acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i], 0, 0, 0);
+      }
+    }
+    if (it + 1 < steps) {
+      __syncthreads();                          // every wave is done with this tile
+      store();
+      __syncthreads();
+    }
+  }
+
+  const int RSC = 4 * a.Cs;
+  float* out = a.ws + (size_t)split * a.Nout * RSC;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < TMW; ++i) {
+      const int k = t * a.Cs + c0 + wave * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
+        out[(size_t)n * RSC + k] = acc[t][i][r];
+      }
+    }
+}
+
 // One launch: block = 16 outputs x 16 split-lanes; lane r sums slabs r, r+16, ...
 // (4 chains), the 16 lane totals are added in fixed order and written in the
 // PyTorch [Nout][Cs][R][S] layout (deterministic, no folding pass).
@@ -340,6 +470,15 @@ int fused_pw(const stf_wgrad_args* a) {
   return c.Wd >= 16 ? 16 : 8;
 }
 
+// ConvT 2x2 / stride 2 fused-tap kernel (x = the 2x larger gradient tensor)
+int fused22_pw(const stf_wgrad_args* a) {
+  static const bool enabled = [] { const char* e = getenv("STF_WGRAD_FUSED"); return !(e && e[0] == '0'); }();
+  const stf_conv_geom& c = a->g;
+  if (!enabled || c.R != 2 || c.S != 2 || c.stride != 2 || c.pad != 0 || c.transposed) return 0;
+  if (c.Hs != 2 * c.Hd || c.Ws != 2 * c.Wd || a->Nout % 64 || c.Cs % 64 || c.Wd < 8) return 0;
+  return c.Wd >= 16 ? 16 : 8;
+}
+
 void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
   ty = (a->g.Hd + 64 / pw - 1) / (64 / pw);
   tx = (a->g.Wd + pw - 1) / pw;
@@ -347,7 +486,7 @@ void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
 }
 
 void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
-  if (const int pw = fused_pw(a)) {
+  if (const int pw = fused_pw(a) ? fused_pw(a) : fused22_pw(a)) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
     const long tiles = (long)(a->Nout / 64) * (a->g.Cs / 64);
@@ -382,7 +521,8 @@ extern "C" int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_b
 }
 
 extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
-  if (const int pw = fused_pw(a)) return pw == 16 ? "wgrad3x3_kernel<16>" : "wgrad3x3_kernel<8>";
+  if (const int pw = fused_pw(a)) return pw == 16 ? "wgrad3x3_kernel<16, 0>" : "wgrad3x3_kernel<8, 0>";
+  if (const int pw = fused22_pw(a)) return pw == 16 ? "wgrad2x2s2_kernel<16>" : "wgrad2x2s2_kernel<8>";
   if (big_tile(a)) return "wgrad_kernel<128, 128, 32, false>";
   return a->g.Cs % 64 == 0 ? "wgrad_kernel<64, 64, 64, false>" : "wgrad_kernel<64, 64, 64, true>";
 }
@@ -414,6 +554,14 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((wgrad3x3_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else
       hipLaunchKernelGGL((wgrad3x3_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+  } else if (const int pw22 = fused22_pw(a)) {
+    int ty, tx, nt;
+    fused_tiles(a, pw22, ty, tx, nt);
+    dim3 grid(splits, a->Nout / 64, c.Cs / 64);
+    if (pw22 == 16)
+      hipLaunchKernelGGL((wgrad2x2s2_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else
+      hipLaunchKernelGGL((wgrad2x2s2_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt);
   } else if (big_tile(a)) {
     dim3 grid(splits, a->Nout / 128, rsc / 128);
     hipLaunchKernelGGL((wgrad_kernel<128, 128, 32, false>), grid, dim3(NT), 0, s, w);

@@ -346,3 +346,17 @@ def test_pack_weights_batched_matches_single():
         single = nhwc.pack_weight(w, mode, cpad)
         assert torch.equal(b, single)
         assert not torch.equal(b, f)
+
+
+@pytest.mark.parametrize("n,cin,cout,h", [(2, 256, 128, 16), (3, 128, 64, 12), (1, 64, 64, 40)])
+def test_wgrad_convT2x2_fused(n, cin, cout, h):
+    """Fused 4-tap ConvTranspose2d(2, 2) weight gradient (incl. ragged pixel tiles)."""
+    from stfunet import nhwc
+    x = bfr(torch.randn(n, cin, h, h, device=DEV))
+    w = torch.randn(cin, cout, 2, 2, device=DEV).requires_grad_(True)
+    y = F.conv_transpose2d(x, w, stride=2)
+    dy = bfr(torch.randn_like(y))
+    y.backward(dy)
+    dw = torch.empty(cin * cout * 4, device=DEV)
+    nhwc.wgrad(feat_from(x), feat_from(dy), 2, 2, 2, 0, dw)
+    assert rel(dw.view_as(w), w.grad) < 2e-3
