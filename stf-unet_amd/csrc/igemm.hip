@@ -395,7 +395,10 @@ STF_DEV int swzk(int row, int kc) {
   else return kc ^ ((row >> 1) & 7);
 }
 
-template <int BM, int BN, int WM, int WN, int BKK, int STAGES, bool TRANS, bool SCATTER, int EPI>
+// C8: 8-channel sources (network inputs): a 16-B chunk is one whole tap, so
+// every lane gathers its own tap (k-step = 4 taps at BKK 32); K need not be a
+// multiple of BKK (k >= K masked)
+template <int BM, int BN, int WM, int WN, int BKK, int STAGES, bool TRANS, bool SCATTER, int EPI, bool C8 = false>
 __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dma_kernel(Geo a, uint32_t src_bytes) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     bkc[i] = swzk<BKK>(row, slot);
   }
   constexpr uint32_t BAD = 0xFFFFFFF0u;
-  const int KT = a.K / BKK;
+  const int KT = C8 ? (a.K + BKK - 1) / BKK : a.K / BKK;
   int tr = 0, ts = 0, tc = 0;                           // tap / channel cursor of the next K step to issue
 
   auto issue = [&](int kt) {
@@ -460,6 +463,17 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     for (int i = 0; i < LA; ++i) {
       int ys, xs;
       bool ok = rok[i];
+      if (C8) {
+        const int tap = (kt * BKK) / 8 + akc[i], r = tap / a.S, s_ = tap - r * a.S;
+        ys = ry[i] + r;
+        xs = rx[i] + s_;
+        ok = ok && tap < a.R * a.S && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws;
+        const uint32_t off = ok ? (uint32_t)(((rbase[i] + ys * a.Ws + xs) * a.scs) * 2) : BAD;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs_src, (__attribute__((address_space(3))) void*)(st + (wave * (BM / NW) + i * RPI) * ROWB), 16, off, 0,
+            0, 0);
+        continue;
+      }
       if (TRANS) {
         const int ty = ry[i] - tr, tx = rx[i] - ts;
         if (a.st == 2) { ok = ok && !(ty & 1) && !(tx & 1); ys = ty >> 1; xs = tx >> 1; }
@@ -475,7 +489,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     const int k0 = kt * BKK;
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const bool ok = bn_[i] < a.Nout;
+      const bool ok = bn_[i] < a.Nout && (!C8 || k0 + bkc[i] * 8 < a.K);
       const uint32_t off = ok ? (uint32_t)((bn_[i] * a.K + k0 + bkc[i] * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs_wgt, (__attribute__((address_space(3))) void*)(st + BM * ROWB + (wave * (BN / NW) + i * RPI) * ROWB),
@@ -856,6 +870,8 @@ bool dma_enabled() {
 char choose(const stf_igemm_args* a, bool dma_ok) {
   const stf_conv_geom& c = a->g;
   const bool plain = !a->lstm && !a->scatter2x2 && !c.transposed;
+  if (dma_enabled() && dma_ok && plain && c.Cs == 8 && forced_cfg() != 'R')   // 8-channel network inputs
+    return a->Nout <= 64 ? 'e' : 'a';
   if (!dma_enabled() || !dma_ok || c.Cs % 32) return 'R';
   const char f = forced_cfg();
   const bool bk64 = c.Cs % 64 == 0;
@@ -883,6 +899,8 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
 
 Cfg cfg_of(char k) {
   switch (k) {
+    case 'a': return CFG_A;
+    case 'e': return CFG_E;
     case 'B': return CFG_B;
     case 'C': return CFG_C;
     case 'D': return CFG_D;
@@ -892,11 +910,14 @@ Cfg cfg_of(char k) {
 }
 
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
-void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, uint32_t src_bytes, hipStream_t s) {
+void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, bool c8, uint32_t src_bytes, hipStream_t s) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
 #define STF_D(TR, SCA, E) \
   hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, TR, SCA, E>), grid, block, 0, s, g, src_bytes)
-  if (lstm) STF_D(false, false, 1);
+  if (c8)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 0, true>), grid, block, 0, s, g,
+                       src_bytes);
+  else if (lstm) STF_D(false, false, 1);
   else if (scatter) STF_D(false, true, 0);
   else if (trans) STF_D(true, false, 0);
   else STF_D(false, false, 0);
@@ -981,11 +1002,13 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
       if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0>", HALO_PW);
       else snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0>", HALO_PW);
       break;
-    case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d>", tr, sc, epi); break;
-    case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d>", tr, sc, epi); break;
-    case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, 0>", sc); break;
-    case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, 0>", sc); break;
-    case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, 0>", sc); break;
+    case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
+    case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
+    case 'a': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, false, false, 0, true>"); break;
+    case 'e': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, false, false, 0, true>"); break;
+    case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, 0, false>", sc); break;
+    case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, 0, false>", sc); break;
+    case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, 0, false>", sc); break;
     default: {
       const bool small = (a->Nout <= 64 && !a->lstm);
       snprintf(buf, sizeof buf, "igemm_kernel<%s, %s, %s, %s, %d>", small ? "256, 64, 4, 1" : "128, 128, 2, 2",
@@ -1045,8 +1068,10 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
     return 0;
   }
   switch (k) {
-    case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
-    case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, src_bytes, s); break;
+    case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
+    case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
+    case 'a': launch_dma<128, 128, 2, 2, 32, 4>(g, false, false, false, true, src_bytes, s); break;
+    case 'e': launch_dma<256, 64, 4, 1, 32, 4>(g, false, false, false, true, src_bytes, s); break;
     case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, a->scatter2x2, src_bytes, s); break;
     case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, a->scatter2x2, src_bytes, s); break;
     case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, a->scatter2x2, src_bytes, s); break;

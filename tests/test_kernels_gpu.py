@@ -38,7 +38,8 @@ def _seed():
     torch.manual_seed(0)
 
 
-@pytest.mark.parametrize("cin,cout,H,stride,R", [(64, 128, 16, 1, 3), (8, 64, 32, 1, 3), (128, 64, 16, 1, 3),
+@pytest.mark.parametrize("cin,cout,H,stride,R", [(64, 128, 16, 1, 3), (8, 64, 32, 1, 3), (8, 64, 20, 2, 7),
+                                                  (8, 128, 18, 1, 3), (128, 64, 16, 1, 3),
                                                   (64, 128, 16, 2, 3), (64, 128, 16, 2, 1), (32, 32, 8, 1, 3),
                                                   (256, 512, 8, 1, 3)])
 def test_conv_forward_stats_and_dgrad(cin, cout, H, stride, R):
