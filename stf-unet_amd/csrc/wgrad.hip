@@ -439,22 +439,45 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
     }
 }
 
-// One launch: block = 16 outputs x 16 split-lanes; lane r sums slabs r, r+16, ...
-// (4 chains), the 16 lane totals are added in fixed order and written in the
-// PyTorch [Nout][Cs][R][S] layout (deterministic, no folding pass).
+// One launch, deterministic: a block owns 64 consecutive outputs; thread (r, c)
+// (16 split-lanes r x 16 column threads c) sums slabs r, r+16, ... of outputs
+// 4c..4c+3 with float4 loads (a wave reads 4 slabs x 256 contiguous bytes), the
+// 16 lane totals are added in fixed order, and the result is written in the
+// PyTorch [Nout][Cs][R][S] layout.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Nout, int R,
                                                            int S, int Cs, float* __restrict__ out) {
-  __shared__ double red[256];
+  __shared__ double red[16][65];
   const int RSC = R * S * Cs;
-  const long total = (long)Nout * RSC;
-  const long idx = blockIdx.x * 16L + (threadIdx.x & 15);
-  const bool ok = idx < total;
-  const double v = stf::fold16_partial(ws, ok ? splits : 0, total, ok ? idx : 0, ok);
-  const double t = stf::fold16_finish(v, red);
-  if (ok && (threadIdx.x >> 4) == 0) {
-    const int n = (int)(idx / RSC), rem = (int)(idx - (long)n * RSC);
-    const int tap = rem / Cs, c = rem - tap * Cs;
-    out[((long)n * Cs + c) * (R * S) + tap] = (float)t;
+  const long total = (long)Nout * RSC;                 // multiple of 8
+  const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const long e0 = blockIdx.x * 64L + c * 4;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (e0 < total) {
+    int k = r;
+    for (; k + 16 < splits; k += 32) {                 // two slabs in flight
+      const float4 u = *reinterpret_cast<const float4*>(ws + (long)k * total + e0);
+      const float4 v = *reinterpret_cast<const float4*>(ws + (long)(k + 16) * total + e0);
+      acc[0] += (double)u.x + v.x; acc[1] += (double)u.y + v.y;
+      acc[2] += (double)u.z + v.z; acc[3] += (double)u.w + v.w;
+    }
+    for (; k < splits; k += 16) {
+      const float4 u = *reinterpret_cast<const float4*>(ws + (long)k * total + e0);
+      acc[0] += u.x; acc[1] += u.y; acc[2] += u.z; acc[3] += u.w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[r][c * 4 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const long idx = blockIdx.x * 64L + threadIdx.x;
+    if (idx < total) {
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t += red[q][threadIdx.x];
+      const int n = (int)(idx / RSC), rem = (int)(idx - (long)n * RSC);
+      const int tap = rem / Cs, ch = rem - tap * Cs;
+      out[((long)n * Cs + ch) * (R * S) + tap] = (float)t;
+    }
   }
 }
 
@@ -579,7 +602,8 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
 extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs, float* out,
                                 stf_stream_t stream) {
   const long total = (long)Nout * R * S * Cs;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, (hipStream_t)stream, ws,
+  if (total % 8 || ((uintptr_t)ws & 15)) return STF_EINVAL;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, (hipStream_t)stream, ws,
                      splits, Nout, R, S, Cs, out);
   STF_CHECK_LAUNCH();
   return 0;
