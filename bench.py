@@ -38,8 +38,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)      # >= 50 timed after >= 10 warm-up
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="unet", choices=["unet", "stf"],
                     help="unet = BASELINE configs[1] (default); stf = configs[2] (T=8, B=16)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (unet 64, stf 16)")
@@ -87,6 +87,27 @@ def roofline(kt, workload, batch, census):
             "algorithmic_tflop_per_launch": round(k["flops"] / k["launches"] / 1e12, 6),
             "all_conv_gemm_kernels_census_step": {
                 "ms": round(gemm_ms, 3), "tflops": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else 0.0}}
+
+
+def doubleconv_report(blocks):
+    """MFMA utilisation of each UNet DoubleConv in the census training step
+    (north star: >= 70 % on DoubleConv at 256x256; SURVEY 8(d) names dec1
+    (128->64, 64->64) as the fair target).  conv = its conv kernels only (fwd,
+    dgrad, wgrad); block = everything the block launches (incl. BN/ReLU/pool
+    passes) from the first to the last kernel of its forward / backward."""
+    out = {}
+    for name in sorted({t.rsplit(".", 1)[0] for t in blocks}):
+        parts = [blocks[t] for t in (f"{name}.fwd", f"{name}.bwd") if t in blocks]
+        fl = sum(p["flops"] for p in parts)
+        cms = sum(p["conv_ms"] for p in parts)
+        bms = sum(p["block_ms"] for p in parts)
+        if cms <= 0 or bms <= 0:
+            continue
+        ct, bt = fl / (cms * 1e-3) / 1e12, fl / (bms * 1e-3) / 1e12
+        out[name] = {"conv_tflops": round(ct, 1), "conv_mfma_frac": round(ct / MFMA_BF16_PEAK_TFLOPS, 3),
+                     "block_tflops": round(bt, 1), "block_mfma_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 3),
+                     "conv_ms": round(cms, 3), "block_ms": round(bms, 3)}
+    return out
 
 
 def cpu_baseline(args):
@@ -194,13 +215,14 @@ def main():
     # warmup; its last step is a census (every conv-GEMM launch timed) that picks
     # the dominant kernel, and only that kernel is instrumented in the timed
     # region (per-launch events on every kernel perturb a host-bound step)
-    census = {}
+    census, blocks = {}, {}
     for i in range(args.warmup):
         if i == args.warmup - 1 and not args.no_kernel_timer:
             nhwc.TIMER = nhwc.KernelTimer()
         loss = train_step(i)
         if nhwc.TIMER is not None:
             census = nhwc.TIMER.summary()
+            blocks = nhwc.TIMER.tag_summary()
             nhwc.TIMER = None
     torch.cuda.synchronize()
     if world > 1:
@@ -253,6 +275,7 @@ def main():
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
             "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
             "roofline": roof,
+            "doubleconv": doubleconv_report(blocks),
             "kernels_census_step": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in d.items()}
                                     for k, d in census.items()},
             "last_loss": round(last_loss, 5),

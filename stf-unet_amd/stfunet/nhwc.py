@@ -31,9 +31,42 @@ class KernelTimer:
     def __init__(self, only=None):
         self.rec = {}
         self.only = only
+        self.tags = {}       # tag -> {"conv": [(ev0, ev1, flops)], "block": [(ev0, ev1)]}
 
     def wants(self, name):
         return self.only is None or name == self.only
+
+    def block(self, tag):
+        """Context manager: events around a whole program block (e.g. one DoubleConv
+        forward or backward); conv launches inside are also summed under ``tag``."""
+        timer = self
+
+        class _Blk:
+            def __enter__(self):
+                global TIMER_TAG
+                self.prev = TIMER_TAG
+                TIMER_TAG = tag
+                self.ev = timer.begin()
+
+            def __exit__(self, *exc):
+                global TIMER_TAG
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(torch.cuda.current_stream())
+                timer.tags.setdefault(tag, {"conv": [], "block": []})["block"].append((self.ev, ev1))
+                TIMER_TAG = self.prev
+        return _Blk()
+
+    def tag_summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for tag, d in self.tags.items():
+            cms = sum(a.elapsed_time(b) for a, b, _ in d["conv"])
+            cfl = sum(f for _, _, f in d["conv"])
+            bms = sum(a.elapsed_time(b) for a, b in d["block"])
+            out[tag] = dict(conv_ms=cms, block_ms=bms, flops=cfl,
+                            conv_tflops=cfl / (cms * 1e-3) / 1e12 if cms > 0 else 0.0,
+                            block_tflops=cfl / (bms * 1e-3) / 1e12 if bms > 0 else 0.0)
+        return out
 
     def begin(self):
         ev = torch.cuda.Event(enable_timing=True)
@@ -44,6 +77,8 @@ class KernelTimer:
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record(torch.cuda.current_stream())
         self.rec.setdefault(family, []).append((ev0, ev1, flops))
+        if TIMER_TAG is not None:
+            self.tags.setdefault(TIMER_TAG, {"conv": [], "block": []})["conv"].append((ev0, ev1, flops))
 
     def summary(self):
         torch.cuda.synchronize()
@@ -57,6 +92,16 @@ class KernelTimer:
 
 
 TIMER = None   # set to a KernelTimer to instrument igemm / wgrad launches
+TIMER_TAG = None
+
+
+def timed_block(tag):
+    """KernelTimer.block(tag) when a full (census) timer is active, else a no-op."""
+    t = TIMER
+    if t is not None and t.only is None:
+        return t.block(tag)
+    import contextlib
+    return contextlib.nullcontext()
 _NAMES = {}    # launch signature -> device kernel name (stf_*_kernel_name)
 
 

@@ -486,6 +486,7 @@ class _STFFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits):
         prog = ctx.prog
+        dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
         prog.backward(ctx.saved, dlogits)
         ctx.saved = None

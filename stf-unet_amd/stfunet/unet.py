@@ -46,11 +46,20 @@ class _Saved:
 class DoubleConvProgram:
     """Forward/backward schedule of one DoubleConv block on NHWC buffers."""
 
-    def __init__(self, blk):
+    def __init__(self, blk, name=""):
         self.blk = blk
         self.cout = blk[0].out_channels
+        self.name = name
 
     def forward(self, src: Feat, training, need_bwd, out: Feat = None, pooled: Feat = None):
+        with nhwc.timed_block(f"{self.name}.fwd"):
+            return self._forward(src, training, need_bwd, out, pooled)
+
+    def backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None):
+        with nhwc.timed_block(f"{self.name}.bwd"):
+            return self._backward(s, grads, need_dsrc, dz, dpool, dy2)
+
+    def _forward(self, src: Feat, training, need_bwd, out: Feat = None, pooled: Feat = None):
         conv1, bn1, conv2, bn2 = self.blk[0], self.blk[1], self.blk[3], self.blk[4]
         C, dev = self.cout, src.buf.device
         s = _Saved()
@@ -70,7 +79,7 @@ class DoubleConvProgram:
         s.y1, s.a1, s.y2 = y1, a1, y2
         return s if need_bwd else None
 
-    def backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None):
+    def _backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None):
         """Either (dz and/or dpool) w.r.t. the block output, or dy2 (grad w.r.t.
         the raw second conv output, when the BN backward was fused upstream)."""
         conv1, bn1, conv2, bn2 = self.blk[0], self.blk[1], self.blk[3], self.blk[4]
@@ -104,10 +113,12 @@ class UNetProgram:
     def __init__(self, model):
         self.m = model
         self.packs = nhwc.PackCache()
-        self.levels = [DoubleConvProgram(b) for b in (model.enc1, model.enc2, model.enc3, model.enc4)]
-        self.bott = DoubleConvProgram(model.bottleneck)
+        self.levels = [DoubleConvProgram(b, f"enc{i}") for i, b in
+                       enumerate((model.enc1, model.enc2, model.enc3, model.enc4), start=1)]
+        self.bott = DoubleConvProgram(model.bottleneck, "bottleneck")
         self.ups = [model.up4, model.up3, model.up2, model.up1]
-        self.decs = [DoubleConvProgram(b) for b in (model.dec4, model.dec3, model.dec2, model.dec1)]
+        self.decs = [DoubleConvProgram(b, f"dec{i}") for i, b in
+                     zip((4, 3, 2, 1), (model.dec4, model.dec3, model.dec2, model.dec1))]
         self.flat = FlatParams(model)
         # grad_ready_hook(begin): flat-gradient elements [begin, numel) are final.  Backward
         # finishes blocks in exactly the reverse of registration (= flat) order, so the
@@ -251,6 +262,7 @@ class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits):
         prog = ctx.prog
+        dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
         prog.backward(ctx.saved, dlogits)
         ctx.saved = None

@@ -172,3 +172,30 @@ def test_two_training_steps_vs_oracle():
     # and the moments were really updated through the flat kernel
     st = opt.state[named["out_conv.weight"]]
     assert int(st["step"].item()) == 2 and st["exp_avg"].abs().sum().item() > 0
+
+
+def test_autocast_gradscaler_step():
+    """The reference trains under torch.amp.autocast + GradScaler (train.py:240,
+    train_and_eval.py:389-401): the drop-in must train identically there -- its
+    forward is explicit bf16 kernels, logits stay fp32, the scaled gradient flows
+    into the flat .grad views, unscale_/inf-check/step work on them."""
+    from stfunet import engine
+    from stfunet.optim import AdamW
+    batches = [dce_case(21, 2, 8, 64, 64), dce_case(22, 2, 8, 64, 64)]
+    finals = []
+    for use_scaler in (False, True):
+        model, _ = _model(8, seed=7)
+        opt = AdamW(list(model.parameters()), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
+        sched = engine.create_lr_scheduler(opt, 2, 3, warmup=True)
+        scaler = torch.amp.GradScaler("cuda") if use_scaler else None
+        loss, _ = engine.train_one_epoch(model, opt, batches, torch.device(DEV), 0, 2, lr_scheduler=sched,
+                                         print_freq=100, scaler=scaler)
+        assert np.isfinite(loss)
+        if scaler is not None:
+            assert scaler.get_scale() == 65536.0 * 1.0          # no inf/nan step skipped
+        finals.append((loss, {k: v.detach().clone() for k, v in model.named_parameters()}))
+    (l0, p0), (l1, p1) = finals
+    assert abs(l0 - l1) < 1e-3
+    for k in p0:
+        d = (p0[k] - p1[k]).abs().max().item()
+        assert d <= 2.2 * 2e-3 + 1e-6, (k, d)
