@@ -574,7 +574,11 @@ STF_DEV int swzh(int row, int kc) { return kc ^ ((row >> 1) & 2); }
 // NW waves x 64 pixels = PH x PW tile; STAGES = 2: one 8-wave workgroup per CU
 // with a 2-stage ring; STAGES = 1: two 4-wave workgroups per CU, single stage
 // each, so one workgroup's DMA wait and epilogue overlap the other's MFMAs.
-template <int PH, int PW, int NW, int STAGES, int DIAG>
+// DIRECT: weight rows are fetched in the permuted order
+// row j*16 + fk*4 + r <- channel (j>>1)*32 + fk*8 + (j&1)*4 + r, so a lane's
+// accumulators of fragments (0,1) and (2,3) are 8 consecutive channels each and
+// the epilogue stores 16-B chunks straight from registers (no LDS staging).
+template <int PH, int PW, int NW, int STAGES, int DIAG, bool DIRECT = false>
 __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes,
                                                                                     int TY, int TX, int per, int rem) {
   constexpr int NTH = 64 * NW, BN = 64, RPI = 16;       // 64-B rows: 16 per 1-KiB DMA instruction
@@ -628,7 +632,10 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
-      const int tap = wr >> 6, n = nt * BN + (wr & 63);
+      const int wrow = wr & 63;
+      const int tap = wr >> 6,
+                n = nt * BN + (DIRECT ? ((wrow >> 5) * 32 + ((wrow >> 2) & 3) * 8 + ((wrow >> 4) & 1) * 4 + (wrow & 3))
+                                      : wrow);
       const bool ok = live && wr < 9 * BN;
       const uint32_t off = ok ? (uint32_t)(((size_t)n * a.K + tap * a.Cs + cc * 32 + swzh(wr, slot) * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -679,7 +686,8 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
         const int nt = cit / ntiles;
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          bv[j] = __builtin_amdgcn_raw_buffer_load_b128(rs_bias, (nt * BN + j * 16 + fk * 4) * 4, 0, 0);
+          bv[j] = __builtin_amdgcn_raw_buffer_load_b128(
+            rs_bias, (nt * BN + (DIRECT ? (j >> 1) * 32 + fk * 8 + (j & 1) * 4 : j * 16 + fk * 4)) * 4, 0, 0);
       }
     };
     if constexpr (STAGES == 2) {
@@ -724,6 +732,95 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+    }
+    if (DIRECT && ccc + 1 == CC) {
+      // ---- direct epilogue: lane (fr, fk) holds pixel p's channels 8fk..8fk+7 (fragments
+      // 0,1) and 32+8fk.. (2,3); invalid pixels get an out-of-range offset, every lane
+      // issues exactly NSTORE = 8 stores (TM x 2); BN partial sums by shuffles + one LDS pass
+      const int nt = cit / ntiles, tile = cit - nt * ntiles;
+      const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+      const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
+      const __amdgpu_buffer_rsrc_t rs_dst =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      float ps1[16], ps2[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { ps1[e] = 0.f; ps2[e] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int p = wave * WTM + i * 16 + fr;
+        const int y = ty * PH + p / PW, x = tx * PW + p % PW;
+        const bool ok = y < a.Hd && x < a.Wd;
+        const int m = (img * a.Hd + y) * a.Wd + x;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = nt * BN + h * 32 + fk * 8;
+          float f[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            f[r] = acc[i][2 * h][r] + bv[2 * h][r];
+            f[4 + r] = acc[i][2 * h + 1][r] + bv[2 * h + 1][r];
+          }
+          if (a.accumulate && ok) {
+            float o[8];
+            unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)m * a.dcs + ch), o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += o[e];
+          }
+          const uint4 u = pack8(f);
+          const uint32_t off = ok ? (uint32_t)(((size_t)m * a.dcs + ch) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+          acc[i][2 * h] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[i][2 * h + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (a.stats && ok) {
+            float g[8];
+            unpack8(u, g);                              // statistics of the stored (rounded) values
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { ps1[h * 8 + e] += g[e]; ps2[h * 8 + e] += g[e] * g[e]; }
+          }
+        }
+      }
+      if (a.stats) {
+        // over the 16 pixels of each fragment row group (lanes with equal fk), then over waves
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) {
+            ps1[e] += __shfl_xor(ps1[e], o, 64);
+            ps2[e] += __shfl_xor(ps2[e], o, 64);
+          }
+        char* ot = smem + buf * STAGE;
+        float* red = reinterpret_cast<float*>(ot);      // [NW][2][64]
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
+        if (fr == 0) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int c = (e >> 3) * 32 + fk * 8 + (e & 7);
+            red[(wave * 2 + 0) * 64 + c] = ps1[e];
+            red[(wave * 2 + 1) * 64 + c] = ps2[e];
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (tid < 128) {
+          const int q = tid >> 6, col = tid & 63;
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
+          const int key = (img / ipg) * NTn + nt;
+          if (key != run_key) {
+            if (run_key >= 0) flush();
+            run_key = key;
+            run = 0.f;
+          }
+          run += t;
+        }
+      }
+      ccc = 0;
+      ++cit;
+      epi = true;
+      continue;
     }
     if (++ccc == CC) {
       // ---- epilogue through LDS: the stage just read becomes the output tile
@@ -829,6 +926,11 @@ int halo_variant() {
   return v;
 }
 int halo_ph() { return halo_variant() == 1 ? 8 : 16; }
+// direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad), =2 always
+bool halo_direct(const stf_igemm_args* a) {
+  static const int mode = [] { const char* e = getenv("STF_HALO_DIRECT"); return e ? atoi(e) : 1; }();
+  return halo_variant() == 0 && (mode == 2 || (mode == 1 && !a->stats));
+}
 
 int num_cus() {
   static const int n = [] {
@@ -999,7 +1101,9 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
     case 'H':
-      if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0>", HALO_PW);
+      if (halo_direct(a))
+        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, true>", HALO_PW);
+      else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0>", HALO_PW);
       else snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0>", HALO_PW);
       break;
     case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
@@ -1062,7 +1166,11 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, src_bytes,   \
                          ty, tx, (int)(items / grid), (int)(items % grid));                                      \
   } while (0)
-    if (diag == 2) STF_H(2); else STF_H(0);
+    if (diag == 2) STF_H(2);
+    else if (halo_direct(a))
+      hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 0, true>), dim3(grid), dim3(512), 0, s, g, src_bytes,
+                         ty, tx, (int)(items / grid), (int)(items % grid));
+    else STF_H(0);
 #undef STF_H
     STF_CHECK_LAUNCH();
     return 0;
