@@ -589,7 +589,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
   constexpr int STAGE = (HROWS + WROWS) * 64;
   constexpr int PX = PH * PW, WTM = PX / NW, TM = WTM / 16, TN = BN / 16;
   constexpr int PPP = NTH / 8, NSTORE = PX / PPP;      // epilogue: pixels per pass, stores per lane
-  static_assert(WTM == 64 && PW % 16 == 0 && PX % PPP == 0, "tile");
+  static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE, "epilogue scratch");
   static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
@@ -926,6 +926,12 @@ int halo_variant() {
   return v;
 }
 int halo_ph() { return halo_variant() == 1 ? 8 : 16; }
+// tile width: 32 for W >= 32; 16x16 tiles (32 pixels per wave) for 16 <= W < 32
+int halo_pw(const stf_conv_geom& c) { return (c.Wd >= 32 || halo_variant() == 1) ? HALO_PW : 16; }
+int halo_min_w() {
+  static const int v = [] { const char* e = getenv("STF_HALO_MINW"); return e ? atoi(e) : 16; }();
+  return v;
+}
 // direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad), =2 always
 bool halo_direct(const stf_igemm_args* a) {
   static const int mode = [] { const char* e = getenv("STF_HALO_DIRECT"); return e ? atoi(e) : 1; }();
@@ -981,7 +987,9 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
                        c.Wd == c.Ws && a->Nout % 64 == 0;
   if (f == 'H' && halo_ok) return 'H';
   // auto: the halo kernel for full-size 3x3 layers ('L' = auto over the linear kernels only)
-  if (f == '0' && halo_ok && c.Wd >= 32) return 'H';
+  // (measured, tools/ab_minw.sh: at 16 <= W < 32 the 16x16 halo tile wins up to 256 output
+  // channels, the 256x256 linear tile above that)
+  if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= halo_min_w() && a->Nout <= 256))) return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
     if ((plain || a->scatter2x2) && bk64 && !a->lstm && !c.transposed) return f;
@@ -1066,7 +1074,7 @@ int pick_mtile(const stf_igemm_args* a) {
 
 void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
   ty = (c.Hd + halo_ph() - 1) / halo_ph();
-  tx = (c.Wd + HALO_PW - 1) / HALO_PW;
+  tx = (c.Wd + halo_pw(c) - 1) / halo_pw(c);
 }
 
 // persistent halo grid: one workgroup per CU (160 KiB LDS each)
@@ -1101,7 +1109,9 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
     case 'H':
-      if (halo_direct(a))
+      if (halo_pw(c) == 16)
+        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, 16, 8, 2, 0, %s>", halo_direct(a) ? "true" : "false");
+      else if (halo_direct(a))
         snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, true>", HALO_PW);
       else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0>", HALO_PW);
       else snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0>", HALO_PW);
@@ -1166,7 +1176,14 @@ extern "C" int stf_igemm(const stf_igemm_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, src_bytes,   \
                          ty, tx, (int)(items / grid), (int)(items % grid));                                      \
   } while (0)
-    if (diag == 2) STF_H(2);
+    if (halo_pw(c) == 16) {
+      if (halo_direct(a))
+        hipLaunchKernelGGL((conv3x3_halo_kernel<16, 16, 8, 2, 0, true>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty,
+                           tx, (int)(items / grid), (int)(items % grid));
+      else
+        hipLaunchKernelGGL((conv3x3_halo_kernel<16, 16, 8, 2, 0, false>), dim3(grid), dim3(512), 0, s, g, src_bytes,
+                           ty, tx, (int)(items / grid), (int)(items % grid));
+    } else if (diag == 2) STF_H(2);
     else if (halo_direct(a))
       hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 0, true>), dim3(grid), dim3(512), 0, s, g, src_bytes,
                          ty, tx, (int)(items / grid), (int)(items % grid));

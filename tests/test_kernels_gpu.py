@@ -110,6 +110,8 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     (4, 128, 128, 64, 64, 2, False, 192, 64),    # grouped statistics, source = concat slice
     (2, 32, 128, 20, 96, 1, True, 32, 0),        # one 32-channel chunk, accumulate into dst
     (1, 96, 64, 64, 80, 1, False, 96, 0),        # three chunks
+    (4, 64, 128, 16, 16, 2, False, 64, 0),       # 16x16 tiles (16 <= W < 32), grouped statistics
+    (2, 128, 64, 21, 24, 1, True, 128, 0),       # 16x16 tiles, ragged, accumulate
 ])
 def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
