@@ -60,6 +60,18 @@ typedef struct stf_lstm_epi {
   float* gates;        /* [M][4Ch] activated gates (i, f, g, o), for backward     */
 } stf_lstm_epi;
 
+/* BatchNorm-backward reduction fused into a dgrad: dst receives dz, the gradient
+ * w.r.t. act(BN(y)); the epilogue also produces the partial sums of
+ * stf_bn_bwd_reduce (g = relu ? dz * [y*scale+shift > 0] : dz; sum g, sum g*xhat)
+ * without a separate pass over dz and y.  Affine arrays are [groups][C]. */
+typedef struct stf_bnr_epi {
+  const void* y;       /* bf16 pre-BN activation [M][y_cstride], first channel      */
+  int y_cstride;
+  const float* scale; const float* shift; const float* mean; const float* invstd;
+  int relu;
+  float* partial;      /* [groups][stf_igemm_bnr_tiles][2][C] for stf_bn_bwd_finalize */
+} stf_bnr_epi;
+
 typedef struct stf_igemm_args {
   stf_conv_geom g;
   const void* src;     /* bf16, first used channel                              */
@@ -79,11 +91,15 @@ typedef struct stf_igemm_args {
                        /* (per-time-step BatchNorm of the batched STF encoder)  */
   int accumulate;      /* 1: dst += result (bf16 read-modify-write)             */
   const stf_lstm_epi* lstm; /* non-NULL: LSTM cell epilogue, dst unused          */
+  const stf_bnr_epi* bnr;   /* non-NULL: fused BN-backward reduction (no stats,  */
+                            /* no scatter/LSTM); group_rows = the BN's groups    */
 } stf_igemm_args;
 
 /* Partial-statistics rows per group for these args (the tiling depends on the
  * kernel chosen): size `stats` as groups * stf_igemm_stat_tiles(a) * 2 * Nout. */
 int stf_igemm_stat_tiles(const stf_igemm_args* a);
+/* Partial rows per group stf_igemm writes into bnr->partial for these args. */
+int stf_igemm_bnr_tiles(const stf_igemm_args* a);
 /* Device kernel (template instance, as rocprofv3 names it) these args will run;
  * static thread-local string, for per-kernel timers and profile cross-checks. */
 const char* stf_igemm_kernel_name(const stf_igemm_args* a);

@@ -45,6 +45,28 @@ STF_DEV float wave_sum(float v) {
   return v;
 }
 
+// DPP exchange inside a row of 16 lanes (VALU, no LDS traffic)
+template <int CTRL>
+STF_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Reduce-scatter of 16 values over the 16 lanes of a DPP row: returns, on lane r of
+// the row, the row sum of value r.  Hypercube over the lane masks 15, 7, 3, 1
+// (row_mirror, row_half_mirror, quad_perm [3,2,1,0], quad_perm [1,0,3,2]); each
+// step keeps the half of the values selected by the lane bit that mask flips last.
+STF_DEV float row16_reduce_scatter(const float (&v)[16], int r) {
+  float a[8], b[4], c[2];
+  const bool h3 = r & 8, h2 = r & 4, h1 = r & 2, h0 = r & 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = (h3 ? v[k + 8] : v[k]) + dpp_f<0x140>(h3 ? v[k] : v[k + 8]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b[k] = (h2 ? a[k + 4] : a[k]) + dpp_f<0x141>(h2 ? a[k] : a[k + 4]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) c[k] = (h1 ? b[k + 2] : b[k]) + dpp_f<0x1B>(h1 ? b[k] : b[k + 2]);
+  return (h0 ? c[1] : c[0]) + dpp_f<0xB1>(h0 ? c[0] : c[1]);
+}
+
 STF_DEV double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

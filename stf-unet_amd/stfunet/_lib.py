@@ -27,10 +27,16 @@ class LstmEpi(ctypes.Structure):
     _fields_ = [("c_prev", P), ("c_out", P), ("h_out", P), ("h_cstride", c_int), ("gates", P)]
 
 
+class BnrEpi(ctypes.Structure):
+    _fields_ = [("y", P), ("y_cstride", c_int), ("scale", P), ("shift", P), ("mean", P), ("invstd", P),
+                ("relu", c_int), ("partial", P)]
+
+
 class IgemmArgs(ctypes.Structure):
     _fields_ = [("g", ConvGeom), ("src", P), ("wgt", P), ("Nout", c_int), ("dst", P),
                 ("dst_cstride", c_int), ("bias", P), ("stats", P), ("scatter2x2", c_int),
-                ("group_rows", c_int), ("accumulate", c_int), ("lstm", ctypes.POINTER(LstmEpi))]
+                ("group_rows", c_int), ("accumulate", c_int), ("lstm", ctypes.POINTER(LstmEpi)),
+                ("bnr", ctypes.POINTER(BnrEpi))]
 
 
 class WgradArgs(ctypes.Structure):
@@ -41,6 +47,7 @@ class WgradArgs(ctypes.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "stf_igemm_stat_tiles": (c_int, [ctypes.POINTER(IgemmArgs)]),
+    "stf_igemm_bnr_tiles": (c_int, [ctypes.POINTER(IgemmArgs)]),
     "stf_igemm_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(IgemmArgs)]),
     "stf_wgrad_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(WgradArgs)]),
     "stf_igemm": (c_int, [ctypes.POINTER(IgemmArgs), P]),

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import ConvGeom, IgemmArgs, WgradArgs, call, stream
+from ._lib import BnrEpi, ConvGeom, IgemmArgs, WgradArgs, call, stream
 
 BF16 = torch.bfloat16
 
@@ -255,8 +255,10 @@ def _geom(src: Feat, Hd, Wd, R, S, stride, pad, transposed):
 
 
 def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, bias=None,
-          want_stats=False, scatter2x2=False, groups=1, accumulate=False, lstm=None):
-    """Launch stf_igemm; returns the per-tile stats tensor (or None) and tiles per group."""
+          want_stats=False, scatter2x2=False, groups=1, accumulate=False, lstm=None, bnr=None):
+    """Launch stf_igemm; returns the per-tile stats tensor (or None) and tiles per group.
+    ``bnr`` = (y, BNState, relu): dst is dz = d act(BN(y)); the launch also produces the
+    BN-backward partial sums (stf_bnr_epi), returned in place of the stats."""
     src.check()
     dst.check()
     Hd, Wd = (dst.H // 2, dst.W // 2) if scatter2x2 else (dst.H, dst.W)
@@ -274,6 +276,15 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
                   dst.cs, _p(bias), None, int(scatter2x2), M // groups if groups > 1 else 0, int(accumulate),
                   ctypes.pointer(lstm) if lstm is not None else None)
     stats, tiles = None, 0
+    if bnr is not None:
+        y, st, relu = bnr
+        y.check()
+        assert not want_stats and st.groups == groups and (y.N, y.H, y.W, y.C) == (dst.N, dst.H, dst.W, dst.C)
+        epi = BnrEpi(y.ptr(), y.cs, _p(st.scale), _p(st.shift), _p(st.mean), _p(st.invstd), int(relu), None)
+        a.bnr = ctypes.pointer(epi)
+        tiles = _lib.load().stf_igemm_bnr_tiles(ctypes.byref(a))
+        stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
+        epi.partial = _p(stats)
     if want_stats:
         tiles = _lib.load().stf_igemm_stat_tiles(ctypes.byref(a))
         stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
@@ -281,7 +292,8 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     t = TIMER
     if t is not None:
         name = _kernel_name("stf_igemm_kernel_name", ("i", src.N, src.H, src.W, src.C, Hd, Wd, nout, R, S, stride,
-                                                      pad, transposed, scatter2x2, lstm is not None, groups), a)
+                                                      pad, transposed, scatter2x2, lstm is not None, groups,
+                                                      bnr is not None, want_stats), a)
         if not t.wants(name):
             t = None
     ev = t.begin() if t is not None else None
@@ -292,14 +304,18 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     return stats, tiles
 
 
-def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False):
+def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None):
     """Conv2d input gradient: stride 1 runs as a forward gather over flipped taps
     (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather.
-    ``accumulate``: dx += gradient (residual / multi-consumer tensors)."""
+    ``accumulate``: dx += gradient (residual / multi-consumer tensors).
+    ``bnr`` = (y, BNState, relu): dx feeds the backward of act(BN(y)); returns the
+    fused partial sums and tiles for bn_backward_fused."""
+    groups = bnr[1].groups if bnr is not None else 1
     if stride == 1 and 2 * pad == R - 1 and R == S:
-        igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate)
-    else:
-        igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True, accumulate=accumulate)
+        return igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate, bnr=bnr,
+                     groups=groups)
+    return igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True, accumulate=accumulate,
+                 bnr=bnr, groups=groups)
 
 
 def rows(f: Feat, n0, n):
@@ -452,6 +468,14 @@ def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool:
     else:
         dy = bn_backward_from_partial(g, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=out)
     return (dy, g) if keep_g else dy
+
+
+def bn_backward_fused(dz: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None, relu=True):
+    """Backward of act(BN(y)) when the producer of dz (conv_dgrad with ``bnr``) already
+    reduced the partial sums: finalize + apply, dy written over dz."""
+    assert dz.cs == dz.C and dz.off == 0
+    return bn_backward_from_partial(dz, y, st, bn, part, tiles, dgamma, dbeta, dbias, out=dz if relu else None,
+                                    mask_relu=relu)
 
 
 def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None,

@@ -145,9 +145,10 @@ class ResBlockProgram:
                                    relu=False, out=new_feat(g.N, g.H, g.W, g.C, g.buf.device))
         nhwc.wgrad(dy2, s.a1, 3, 3, 1, 1, gv(self.conv2.weight))
         da1 = new_feat(s.a1.N, s.a1.H, s.a1.W, self.cout, s.a1.buf.device)
-        nhwc.conv_dgrad(dy2, self.conv2.weight, da1, 3, 3, 1, 1)
+        part, tiles = nhwc.conv_dgrad(dy2, self.conv2.weight, da1, 3, 3, 1, 1, bnr=(s.y1, s.bn1, True))
         del dy2
-        dy1 = nhwc.bn_backward(s.y1, s.bn1, self.bn1, gv(self.bn1.weight), gv(self.bn1.bias), dz=da1)
+        dy1 = nhwc.bn_backward_fused(da1, s.y1, s.bn1, self.bn1, part, tiles, gv(self.bn1.weight),
+                                     gv(self.bn1.bias))
         del da1
         nhwc.wgrad(dy1, src, 3, 3, self.stride, 1, gv(self.conv1.weight))
         if self.sc_conv is None:

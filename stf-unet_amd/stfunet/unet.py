@@ -89,8 +89,10 @@ class DoubleConvProgram:
                                    dbias=gv(conv2.bias))
         nhwc.wgrad(dy2, s.a1, 3, 3, 1, 1, gv(conv2.weight))
         da1 = new_feat(s.a1.N, s.a1.H, s.a1.W, self.cout, s.a1.buf.device)
-        nhwc.conv_dgrad(dy2, conv2.weight, da1, 3, 3, 1, 1)
-        dy1 = nhwc.bn_backward(s.y1, s.bn1, bn1, gv(bn1.weight), gv(bn1.bias), dz=da1, dbias=gv(conv1.bias))
+        # dgrad of conv2 also reduces BN1's backward sums (fused epilogue)
+        part, tiles = nhwc.conv_dgrad(dy2, conv2.weight, da1, 3, 3, 1, 1, bnr=(s.y1, s.bn1, True))
+        dy1 = nhwc.bn_backward_fused(da1, s.y1, s.bn1, bn1, part, tiles, gv(bn1.weight), gv(bn1.bias),
+                                     dbias=gv(conv1.bias))
         del da1
         self._wgrad_conv1(dy1, s.src, gv(conv1.weight))
         if not need_dsrc:

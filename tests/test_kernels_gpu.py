@@ -144,6 +144,50 @@ def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     assert rel(dx.dense(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W,groups,relu,acc", [
+    (2, 64, 128, 40, 72, 1, True, False),     # halo 16x32 tiles, ragged edges
+    (4, 128, 64, 24, 20, 2, True, False),     # halo 16x16 tiles, two BN groups
+    (2, 64, 64, 64, 64, 1, False, True),      # plain BN (no ReLU), accumulate
+    (4, 256, 128, 8, 8, 2, True, False),      # linear kernel: separate reduce fallback
+])
+def test_dgrad_fused_bn_backward_reduce(n, cin, cout, H, W, groups, relu, acc):
+    """conv_dgrad with ``bnr``: dz identical to the plain dgrad, and the fused partial
+    sums (g, g*xhat) equal to a separate stf_bn_bwd_reduce pass over the stored dz."""
+    from stfunet import nhwc
+    from stfunet._lib import call, load, stream
+    from stfunet.nhwc import BNState, _p
+    w = bfr(torch.randn(cout, cin, 3, 3, device=DEV) / (cout * 9) ** 0.5)
+    dy = feat_from(bfr(torch.randn(n, cout, H, W, device=DEV)))
+    y = feat_from(bfr(torch.randn(n, cin, H, W, device=DEV) * 2 + 0.5))
+    st = BNState(cin, DEV, n * H * W, groups)
+    st.mean.copy_(torch.randn(groups, cin, device=DEV) * 0.3 + 0.5)
+    st.invstd.copy_(torch.rand(groups, cin, device=DEV) + 0.5)
+    st.scale.copy_(torch.randn(groups, cin, device=DEV))
+    st.shift.copy_(torch.randn(groups, cin, device=DEV) * 0.5)
+    base = bfr(torch.randn(n, cin, H, W, device=DEV))
+    dx0 = feat_from(base) if acc else nhwc.new_feat(n, H, W, cin, DEV)
+    nhwc.conv_dgrad(dy, w.contiguous(), dx0, 3, 3, 1, 1, accumulate=acc)
+    dx = feat_from(base) if acc else nhwc.new_feat(n, H, W, cin, DEV)
+    part, tiles = nhwc.conv_dgrad(dy, w.contiguous(), dx, 3, 3, 1, 1, accumulate=acc, bnr=(y, st, relu))
+    assert torch.equal(dx.buf, dx0.buf)
+    t2 = load().stf_bn_bwd_tiles(n, H, W, cin, groups, 0)
+    ref = torch.empty(groups * t2 * 2 * cin, dtype=torch.float32, device=DEV)
+    call("stf_bn_bwd_reduce", dx.ptr(), dx.cs, None, y.ptr(), y.cs, n, H, W, cin, groups, _p(st.scale),
+         _p(st.shift), _p(st.mean), _p(st.invstd), int(relu), None, 0, None, _p(ref), stream())
+    got = part.view(groups, tiles, 2, cin).double().sum(1)
+    exp = ref.view(groups, t2, 2, cin).double().sum(1)
+    assert rel(got, exp) < 1e-5
+    # and against a direct float64 restatement
+    g = dx.dense().double().view(groups, n // groups, cin, H, W)
+    yy = y.dense().double().view(groups, n // groups, cin, H, W)
+    sc, sh = st.scale.double()[:, None, :, None, None], st.shift.double()[:, None, :, None, None]
+    if relu:
+        g = g * ((yy * sc + sh) > 0)
+    xh = (yy - st.mean.double()[:, None, :, None, None]) * st.invstd.double()[:, None, :, None, None]
+    assert rel(got[:, 0], g.sum((1, 3, 4))) < 1e-5
+    assert rel(got[:, 1], (g * xh).sum((1, 3, 4))) < 1e-5
+
+
 def test_conv_into_concat_slice():
     from stfunet import nhwc
     x = bfr(torch.randn(2, 64, 8, 8, device=DEV))
