@@ -570,9 +570,11 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
 // offsets (r * (PW+2) + s).  Persistent: each workgroup walks a contiguous run
 // of (tile, channel-slice) items through a 2-stage LDS-DMA ring, so the next
 // stage streams in behind the MFMAs and the epilogue.  Rows are 64 B with the
-// chunk swizzle kc ^ ((row >> 1) & 2), conflict-free for ds_read_b128 at ANY
-// row offset (a tap shift moves the 16 rows a fragment reads by 0..2 rows).
-STF_DEV int swzh(int row, int kc) { return kc ^ ((row >> 1) & 2); }
+// chunk swizzle kc ^ ((key >> 1) & 2): for weight rows key = row, for halo rows
+// key = the halo COLUMN, so a tap's row shift dy leaves the swizzle unchanged (an
+// immediate offset).  Both are conflict-free for every ds_read_b128 lane group at
+// any tap shift (checked exhaustively over columns, shifts and row residues).
+STF_DEV int swzh(int key, int kc) { return kc ^ ((key >> 1) & 2); }
 
 // NW waves x 64 pixels = PH x PW tile; STAGES = 2: one 8-wave workgroup per CU
 // with a 2-stage ring; STAGES = 1: two 4-wave workgroups per CU, single stage
@@ -597,7 +599,8 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
   static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar DMA addressing
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
   const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
   const int ntiles = a.N * tpi;                         // items: channel slice major, pixel tile minor
@@ -628,7 +631,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       const int ys = y0 + hy, xs = x0 + hx;
       const bool ok = live && hr < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws;
       const uint32_t off =
-          ok ? (uint32_t)((((img * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hr, slot) * 8) * 2) : BAD;
+          ok ? (uint32_t)((((img * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hx, slot) * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs_src, (__attribute__((address_space(3))) void*)(st + (wave * HI + i) * RPI * 64), 16, off, 0, 0, 0);
     }
@@ -647,11 +650,18 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     }
   };
 
-  int hbase[TM];                                        // halo row of this lane's pixel, tap (0, 0)
+  // byte offset (within a stage) of this lane's halo read for fragment i at tap column dx,
+  // tap row 0: the swizzle is keyed on the halo column, so the tap row dy only adds the
+  // immediate dy * HW * 64 (12 address registers instead of one per (i, tap))
+  int xb[TM][3];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int p = wave * WTM + i * 16 + fr;
-    hbase[i] = (p / PW) * HW + p % PW;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int hx = p % PW + dx;
+      xb[i][dx] = ((p / PW) * HW + hx) * 64 + swzh(hx, fk) * 16;
+    }
   }
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -721,25 +731,52 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     const char* hb = smem + buf * STAGE;
     if (DIAG == 3) { if (++ccc == CC) { ccc = 0; ++cit; } continue; }
     const char* wb = hb + HROWS * 64;
+    // software-pipelined taps: tap t+1's fragments are read while tap t's TM x TN MFMAs
+    // run (double-buffered registers).  The reads are inline-asm ds_read_b128 (kept in
+    // issue order; the compiler otherwise sinks them next to their MFMAs and exposes the
+    // LDS latency) and the wait is explicit: lgkmcnt(TM + TN) leaves exactly the tap-t+1
+    // reads in flight, and it passes tap t's fragments through as operands so no MFMA
+    // can be scheduled above it.  All reads have retired (lgkmcnt(0)) by the last tap.
+    bf16x8 xf[2][TM], wf[2][TN];
+    const uint32_t hb32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)hb;
+    const uint32_t wrow0 = (uint32_t)((HROWS + fr) * 64 + swzh(fr, fk) * 16);    // weight row j*16+fr of tap 0
+    auto rd_tap = [&](int t, int b) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(xf[b][i]) : "v"(hb32 + xb[i][t % 3]), "i"((t / 3) * HW * 64));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)                 // (row >> 1) & 2 of t*64 + j*16 + fr = that of fr
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(wf[b][j]) : "v"(hb32 + wrow0), "i"((t * BN + j * 16) * 64));
+    };
+    rd_tap(0, 0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int toff = (t / 3) * HW + (t % 3);
-      bf16x8 xf[TM], wf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = hbase[i] + toff;
-        xf[i] = *reinterpret_cast<const bf16x8*>(hb + row * 64 + swzh(row, fk) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = t * BN + j * 16 + fr;
-        wf[j] = *reinterpret_cast<const bf16x8*>(wb + row * 64 + swzh(row, fk) * 16);
+      const int b = t & 1;
+      if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
+      // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
+      static_assert(TN == 4 && (TM == 4 || TM == 2), "fragment wait");
+      if constexpr (TM == 4) {
+        if (t + 1 < 9)
+          asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(xf[b][0]), "+v"(xf[b][1]), "+v"(xf[b][2]), "+v"(xf[b][3]),
+                       "+v"(wf[b][0]), "+v"(wf[b][1]), "+v"(wf[b][2]), "+v"(wf[b][3]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xf[b][0]), "+v"(xf[b][1]), "+v"(xf[b][2]), "+v"(xf[b][3]),
+                       "+v"(wf[b][0]), "+v"(wf[b][1]), "+v"(wf[b][2]), "+v"(wf[b][3]));
+      } else {
+        if (t + 1 < 9)
+          asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(xf[b][0]), "+v"(xf[b][1]),
+                       "+v"(wf[b][0]), "+v"(wf[b][1]), "+v"(wf[b][2]), "+v"(wf[b][3]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xf[b][0]), "+v"(xf[b][1]),
+                       "+v"(wf[b][0]), "+v"(wf[b][1]), "+v"(wf[b][2]), "+v"(wf[b][3]));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[b][j], xf[b][i], acc[i][j], 0, 0, 0);
     }
     if (DIRECT && ccc + 1 == CC) {
       // ---- direct epilogue: lane (fr, fk) holds pixel p's channels 8fk..8fk+7 (fragments
@@ -1316,8 +1353,13 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
       if (d == 2) STF_HL(16, 2, false);
       else if (d == 1) STF_HL(16, 1, false);
       else STF_HL(16, 0, false);
-    } else if (diag == 2) STF_H(2);
-    else if (d == 2) STF_HL(HALO_PW, 2, false);
+    } else if (diag == 2) {                        // ablation: no DMA reloads after the first stage
+      if (d == 2) hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 2, 2, false>), dim3(grid), dim3(512), 0,
+                                     s, g, src_bytes, ty, tx, per, rem);
+      else if (d == 1) hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 2, 1, false>), dim3(grid), dim3(512),
+                                          0, s, g, src_bytes, ty, tx, per, rem);
+      else STF_H(2);
+    } else if (d == 2) STF_HL(HALO_PW, 2, false);
     else if (d == 1) STF_HL(HALO_PW, 1, false);
     else STF_H(0);
 #undef STF_HL
