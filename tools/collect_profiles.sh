@@ -1,15 +1,34 @@
 #!/bin/bash
-# Round profile collection (run on the GPU box from the repo root):
-#   kernel-trace stats for the UNet (cfg2) and STF (cfg3) bench steps, and the
-#   two PMC passes (HBM traffic) for cfg2.  Outputs under gpurun_out/prof_<tag>.
+# Round profile collection (GPU box, repo root), all on ONE box so the numbers agree:
+#   1. the bench lines (python bench.py [--model stf], default steps)
+#   2. rocprofv3 --kernel-trace --stats of the SAME commands (per-kernel averages that
+#      the bench line's roofline avg_launch_us is checked against)
+#   3. the two PMC passes (HBM traffic, tools/pmc_passes.sh) per model -> pmc_traffic_*.json
+# Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
 set -e
 tag=${1:-r01}
-out=gpurun_out/prof_$tag
+root=$GRAFT_REPO_ROOT
+out=$root/gpurun_out/prof_$tag
 mkdir -p $out
+timeout -k 10 600 python3 bench.py > $out/bench_unet256_b64.json 2> $out/bench_unet.err
+timeout -k 10 600 python3 bench.py --model stf > $out/bench_stf256_t8_b16.json 2> $out/bench_stf.err
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/unet" -o run -- \
-  python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$out/unet.log" 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/stf" -o run -- \
-  python3 "$GRAFT_REPO_ROOT/bench.py" --model stf --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/$out/stf.log" 2>&1
-cd "$GRAFT_REPO_ROOT"
-bash tools/pmc_passes.sh $out/pmc --steps 3 --warmup 1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/unet -o run -- \
+  python3 $root/bench.py > $out/unet_rocprof_bench.json 2> $out/unet.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stf -o run -- \
+  python3 $root/bench.py --model stf > $out/stf_rocprof_bench.json 2> $out/stf.log
+cd $root
+if [ -z "$SKIP_PMC" ]; then
+bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_unet --steps 3 --warmup 1
+bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_stf --model stf --steps 3 --warmup 1
+python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_unet --batch 64 \
+  --workload "cfg2 UNet(in=8,base_c=64) 256x256 train step" \
+  --command "bash tools/pmc_passes.sh OUT --steps 3 --warmup 1" --json $out/pmc_traffic_unet256_b64.json > $out/pmc_unet256_b64_summary.txt
+python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_stf --batch 16 \
+  --workload "cfg3 STFLSTMUNet(T=8) 256x256 train step" \
+  --command "bash tools/pmc_passes.sh OUT --model stf --steps 3 --warmup 1" --json $out/pmc_traffic_stf256_t8_b16.json > $out/pmc_stf256_t8_b16_summary.txt
+fi
+cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
+cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
+rm -rf $out/unet $out/stf $out/pmc_unet $out/pmc_stf
+ls $out
