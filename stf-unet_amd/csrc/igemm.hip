@@ -33,6 +33,8 @@ struct Geo {
   // fused BN-backward reduction (stf_bnr_epi)
   const uint16_t* bnr_y; int bnr_ycs; const float *bnr_scale, *bnr_shift, *bnr_mean, *bnr_invstd;
   int bnr_relu; float* bnr_part;
+  // stride-2 transposed gather with rows ordered by output parity class (see igemm_dma_kernel)
+  int par;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -148,7 +150,7 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
 // values.  Needs BM*BN*2 + NW*2*BN*4 bytes of LDS (the drained ring).
 template <int BM, int BN, int WM, int WN, bool SCATTER, int NTH>
 STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end, int n0,
-                             int wm, int wn, int tid, char* smem, int tile) {
+                             int wm, int wn, int tid, char* smem, int tile, int pcls = -1) {
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int CPR = BN / 8, RPP = NTH / CPR, PASSES = BM / RPP, NW = WM * WN;
   static_assert(NTH % CPR == 0 && BM % RPP == 0, "epilogue mapping");
@@ -189,6 +191,11 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
       const int img = m / hw, rem = m - img * hw;
       const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
       off = ((size_t)(img * 2 * a.Hd + 2 * yd + (blk >> 1)) * (2 * a.Wd) + 2 * xd + (blk & 1)) * a.dcs + co;
+    } else if (pcls >= 0) {                          // parity-class row -> output pixel
+      const int py = pcls >> 1, px = pcls & 1;
+      const int Hc = (a.Hd - py + 1) >> 1, Wc = (a.Wd - px + 1) >> 1;
+      const int img = m / (Hc * Wc), rem = m - img * (Hc * Wc), u = rem / Wc, v = rem - u * Wc;
+      off = ((size_t)(img * a.Hd + 2 * u + py) * a.Wd + 2 * v + px) * a.dcs + n;
     } else {
       off = (size_t)m * a.dcs + n;
     }
@@ -425,9 +432,29 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int bx = wid / gy, by = wid - bx * gy;
   const int grp = bx / a.tpg, gtile = bx - grp * a.tpg;
-  const int m0 = grp * a.Mg + gtile * BM, n0 = by * BN;
-  const int m_end = min(m0 + BM, min((grp + 1) * a.Mg, a.M));
+  int m0 = grp * a.Mg + gtile * BM, m_end = min(m0 + BM, min((grp + 1) * a.Mg, a.M));
+  const int n0 = by * BN;
   const int sub = lane / CPR, slot = lane % CPR;
+  // Parity mode (stride-2 transposed gather): output pixel (y, x) only receives the taps
+  // r = y + pad (mod 2), s = x + pad (mod 2).  Rows are ordered by class (y & 1, x & 1),
+  // each block lies in one class and walks only that class's taps (1/2/2/4 of the nine
+  // for 3x3, none for the odd classes of 1x1) instead of masking 3/4 of the MFMAs to zero.
+  int pcls = -1, py = 0, px = 0, Hc = 0, Wc = 0, r0 = 0, s0 = 0;
+  if (TRANS && a.par) {
+    int b = gtile;
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      const int c = 3 - ci;                         // (1,1) first: 4 taps, then 2, 2, 1 (shorter tail)
+      const int hc = (a.Hd - (c >> 1) + 1) >> 1, wc = (a.Wd - (c & 1) + 1) >> 1;
+      const int mc = a.N * hc * wc, nb = (mc + BM - 1) / BM;
+      if (pcls < 0) {
+        if (b < nb) { pcls = c; Hc = hc; Wc = wc; m0 = b * BM; m_end = min(m0 + BM, mc); }
+        else b -= nb;
+      }
+    }
+    py = pcls >> 1; px = pcls & 1;
+    r0 = (py + a.pad) & 1; s0 = (px + a.pad) & 1;
+  }
 
   const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_wgt =
@@ -441,9 +468,17 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     const int m = m0 + row;
     rok[i] = m < m_end;
     const int mm = rok[i] ? m : m0;
-    const int hw = a.Hd * a.Wd;
-    const int n = mm / hw, rem = mm - n * hw;
-    const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
+    int n, yd, xd;
+    if (TRANS && a.par) {
+      n = mm / (Hc * Wc);
+      const int rem = mm - n * (Hc * Wc), u = rem / Wc;
+      yd = 2 * u + py; xd = 2 * (rem - u * Wc) + px;
+    } else {
+      const int hw = a.Hd * a.Wd;
+      n = mm / hw;
+      const int rem = mm - n * hw;
+      yd = rem / a.Wd; xd = rem - yd * a.Wd;
+    }
     rbase[i] = n * a.Hs * a.Ws;
     if (TRANS) { ry[i] = yd + a.pad; rx[i] = xd + a.pad; }
     else { ry[i] = yd * a.st - a.pad; rx[i] = xd * a.st - a.pad; }
@@ -457,8 +492,10 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     bkc[i] = swzk<BKK>(row, slot);
   }
   constexpr uint32_t BAD = 0xFFFFFFF0u;
-  const int KT = C8 ? (a.K + BKK - 1) / BKK : a.K / BKK;
-  int tr = 0, ts = 0, tc = 0;                           // tap / channel cursor of the next K step to issue
+  const int tstep = (TRANS && a.par) ? 2 : 1;          // tap stride of the cursor
+  const int KT = C8 ? (a.K + BKK - 1) / BKK
+                    : ((TRANS && a.par) ? ((a.R - r0 + 1) >> 1) * ((a.S - s0 + 1) >> 1) * (a.Cs / BKK) : a.K / BKK);
+  int tr = r0, ts = s0, tc = 0;                         // tap / channel cursor of the next K step to issue
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE;
@@ -489,7 +526,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
           rs_src, (__attribute__((address_space(3))) void*)(st + (wave * (BM / NW) + i * RPI) * ROWB), 16, off, 0, 0,
           0);
     }
-    const int k0 = kt * BKK;
+    const int k0 = C8 ? kt * BKK : (tr * a.S + ts) * a.Cs + tc;
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const bool ok = bn_[i] < a.Nout && (!C8 || k0 + bkc[i] * 8 < a.K);
@@ -499,7 +536,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
           16, off, 0, 0, 0);
     }
     tc += BKK;
-    if (tc == a.Cs) { tc = 0; if (++ts == a.S) { ts = 0; ++tr; } }
+    if (tc == a.Cs) { tc = 0; ts += tstep; if (ts >= a.S) { ts = s0; tr += tstep; } }
   };
 
   f32x4 acc[TM][TN];
@@ -544,7 +581,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (EPI == 0) {
-    staged_epilogue<BM, BN, WM, WN, SCATTER, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx);
+    staged_epilogue<BM, BN, WM, WN, SCATTER, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx, pcls);
   } else {
     int mrow[TM];
 #pragma unroll
@@ -1312,6 +1349,7 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.c_prev = nullptr; g.c_out = nullptr; g.h_out = nullptr; g.hcs = 0; g.gates = nullptr;
   g.bnr_y = nullptr; g.bnr_ycs = 0; g.bnr_scale = g.bnr_shift = g.bnr_mean = g.bnr_invstd = nullptr;
   g.bnr_relu = 0; g.bnr_part = nullptr;
+  g.par = 0;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
@@ -1366,6 +1404,17 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
 #undef STF_H
     STF_CHECK_LAUNCH();
     return 0;
+  }
+  // stride-2 transposed gathers: rows by output parity class, only that class's taps
+  // (STF_TRANS_PAR=0: all nine taps, 3/4 of them masked)
+  static const bool par_on = [] { const char* e = getenv("STF_TRANS_PAR"); return !(e && e[0] == '0'); }();
+  if (par_on && c.transposed && c.stride == 2 && (k == 'A' || k == 'E') && g.Mg == g.M) {
+    const int bmp = cfg_of(k).bm;
+    long blocks = 0;
+    for (int cl = 0; cl < 4; ++cl)
+      blocks += ((long)c.N * ((c.Hd - (cl >> 1) + 1) >> 1) * ((c.Wd - (cl & 1) + 1) >> 1) + bmp - 1) / bmp;
+    g.par = 1;
+    g.tpg = (int)blocks;
   }
   switch (k) {
     case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;

@@ -70,6 +70,34 @@ def test_conv_forward_stats_and_dgrad(cin, cout, H, stride, R):
         assert rel(dx.dense(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W,R,acc", [
+    (2, 64, 128, 15, 17, 3, False),     # odd input sizes: the four parity classes differ in size
+    (4, 128, 256, 32, 32, 3, True),     # several blocks per class, accumulate into dx
+    (2, 64, 128, 13, 16, 1, False),     # 1x1 / stride 2: odd classes get no taps (dx = 0 there)
+    (2, 256, 64, 8, 9, 1, True),        # 1x1 / stride 2, accumulate (odd classes keep dx)
+    (3, 32, 64, 9, 11, 3, False),       # one 32-channel chunk, 256 x 64 tile (Nout <= 64)
+])
+def test_strided_dgrad_parity_classes(n, cin, cout, H, W, R, acc):
+    """Stride-2 input gradient through the transposed gather with rows ordered by output
+    parity class (each class walks only its own taps) vs torch."""
+    from stfunet import nhwc
+    pad = R // 2
+    x = bfr(torch.randn(n, cin, H, W, device=DEV))
+    w = bfr(torch.randn(cout, cin, R, R, device=DEV) / (cin * R * R) ** 0.5)
+    xr = x.clone().requires_grad_(True)
+    y = F.conv2d(xr, w, stride=2, padding=pad)
+    dy = bfr(torch.randn_like(y))
+    y.backward(dy)
+    base = bfr(torch.randn(n, cin, H, W, device=DEV))
+    dx = feat_from(base) if acc else nhwc.new_feat(n, H, W, cin, DEV)
+    nhwc.conv_dgrad(feat_from(dy), w.contiguous(), dx, R, R, 2, pad, accumulate=acc)
+    ref = xr.grad + base if acc else xr.grad
+    assert rel(dx.dense(), ref) < 1e-2
+    if R == 1 and not acc:                  # no tap reaches odd rows / columns
+        assert dx.dense()[:, :, 1::2].abs().max().item() == 0
+        assert dx.dense()[:, :, :, 1::2].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("cin,cout,H,stride,R,pad", [(64, 128, 16, 1, 3, 1), (8, 64, 32, 1, 3, 1),
                                                      (64, 128, 16, 2, 3, 1), (64, 64, 16, 2, 1, 0),
                                                      (256, 256, 8, 1, 3, 1), (8, 64, 16, 2, 7, 3)])
