@@ -631,6 +631,13 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
   constexpr int STAGE = (HROWS + WROWS) * 64;
   constexpr int PX = PH * PW, WTM = PX / NW, TM = WTM / 16, TN = BN / 16;
   constexpr int PPP = NTH / 8, NSTORE = PX / PPP;      // epilogue: pixels per pass, stores per lane
+  // next stage's DMA (STAGES == 2): even waves at the stage start, odd waves after tap 4.
+  // DIAG 4 cycle buckets (tools/halo_timeline.py, 256^2 64->64): with every wave issuing
+  // at once a third of the wave time is spent stalled issuing LDS-DMA; staggered, one wave
+  // of each SIMD computes while the other issues (-8 % cycles).  Spreading every wave's
+  // instructions over the taps only moves the stall into the taps: the DMA path itself
+  // is the limit, fewer bytes per FLOP is what would help.
+  constexpr bool STAGGER = STAGES == 2 && NW == 8;
   static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE && NW * 3 * 64 * 4 * 2 + PX * 128 <= STAGE, "epilogue scratch");
   static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
@@ -656,13 +663,15 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       (void*)a.bias, 0, a.bias ? (uint32_t)a.Nout * 4 : 0u, 0x00020000);
 
   // live = false: a dummy stage (all lanes out of range) so every iteration issues the same DMA count
-  auto issue = [&](int item, int cc, int buf, bool live) {
+  // DMA instructions k0 .. k1-1 of this wave's HI halo + WI weight instructions
+  auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1) {
     const int nt = item / ntiles, tile = item - nt * ntiles;
     const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
     char* st = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < HI; ++i) {
+      if (i < k0 || i >= k1) continue;
       const int hr = (wave * HI + i) * RPI + sub;
       const int hy = hr / HW, hx = hr - hy * HW;
       const int ys = y0 + hy, xs = x0 + hx;
@@ -674,6 +683,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     }
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
+      if (HI + i < k0 || HI + i >= k1) continue;
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
@@ -686,6 +696,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
           0, 0);
     }
   };
+  auto issue = [&](int item, int cc, int buf, bool live) { issue_part(item, cc, buf, live, 0, HI + WI); };
 
   // byte offset (within a stage) of this lane's halo read for fragment i at tap column dx,
   // tap row 0: the swizzle is keyed on the halo column, so the tap row dy only adds the
@@ -728,8 +739,18 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
         sbuf[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = 0.f;
   }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
+  // DIAG 4: per-wave cycle buckets (s_memtime) -- DMA wait, barrier, DMA issue, taps, epilogue
+  uint64_t tb[5] = {0, 0, 0, 0, 0}, tprev = 0;
+  auto stamp = [&](int k) {
+    if constexpr (DIAG == 4) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if (k >= 0) tb[k] += t - tprev;
+      tprev = t;
+    }
+  };
   for (int s = 0; s < S; ++s) {
     const int buf = STAGES == 2 ? (s & 1) : 0;
+    stamp(-1);
     f32x4 bv[TN];
     auto load_bias = [&]() {
       // bias of this lane's 16 accumulator channels, loaded BEFORE the next DMA so
@@ -750,12 +771,19 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       // (issued after it, stores and loads retire in order) may stay in flight
       if (epi) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamp(0);
       epi = false;
       __builtin_amdgcn_s_barrier();
+      stamp(1);
       load_bias();
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
-      issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
+      // even waves issue the next stage's DMA now, odd waves after tap 4: the address
+      // path takes ~300 cycles per 1-KiB LDS-DMA instruction under load, and with all
+      // eight waves issuing at once both waves of a SIMD stalled together (DIAG 4: a third
+      // of the time); staggered, one wave of each SIMD computes while the other issues
+      if (!STAGGER || !(wave & 1)) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
+      stamp(2);
     } else {
       // single stage: every wave is done with the buffer, refill it, wait
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -791,6 +819,9 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int b = t & 1;
+      if constexpr (STAGGER) {
+        if (t == 4 && (wave & 1)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1));
+      }
       if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
       // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
       static_assert(TN == 4 && (TM == 4 || TM == 2), "fragment wait");
@@ -815,6 +846,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[b][j], xf[b][i], acc[i][j], 0, 0, 0);
     }
+    stamp(3);
     if (DIRECT && ccc + 1 == CC) {
       // ---- direct epilogue: lane (fr, fk) holds pixel p's channels 8fk..8fk+7 (fragments
       // 0,1) and 32+8fk.. (2,3).  Order: pack the accumulators (64 fp32 -> 32 bf16x2
@@ -977,6 +1009,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
           run += t;
         }
       }
+      stamp(4);
       ccc = 0;
       ++cit;
       epi = true;
@@ -1081,6 +1114,13 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     }
   }
   if (sbuf && tid < 128 && run_key >= 0) flush();
+  if constexpr (DIAG == 4) {                           // a.stats doubles as the [grid][NW][8] u64 buffer
+    if (lane == 0) {
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(a.stats) + (blockIdx.x * NW + wave) * 8;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) d[k] = tb[k];
+    }
+  }
 }
 
 constexpr int HALO_PW = 32;
@@ -1391,6 +1431,9 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
       if (d == 2) STF_HL(16, 2, false);
       else if (d == 1) STF_HL(16, 1, false);
       else STF_HL(16, 0, false);
+    } else if (diag == 4) {                        // cycle buckets (tools/halo_timeline.py), no statistics
+      hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 4, 1, false>), dim3(grid), dim3(512), 0, s, g,
+                         src_bytes, ty, tx, per, rem);
     } else if (diag == 2) {                        // ablation: no DMA reloads after the first stage
       if (d == 2) hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, 2, 2, false>), dim3(grid), dim3(512), 0,
                                      s, g, src_bytes, ty, tx, per, rem);

@@ -12,6 +12,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstfunet_hip.so")
+# A/B measurements: STF_LIB points at another build of the same library (tools/ab_lib.sh)
+LIB_PATH = os.environ.get("STF_LIB", LIB_PATH)
 
 c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
                                                 ctypes.c_size_t, ctypes.c_int64)
