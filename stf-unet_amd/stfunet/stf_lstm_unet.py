@@ -249,6 +249,17 @@ class STFProgram:
         self.final_res = ResBlockProgram(fr.conv_block[0], fr.conv_block[1], fr.conv_block[3], fr.conv_block[4])
         self.lstms = [m.lstm1, m.lstm2, m.lstm3, m.lstm4]
         self.lstm_progs = [LSTMProgram(lstm) for lstm in self.lstms]
+        self._side = None
+
+    def side_streams(self, dev):
+        """One HIP stream per LSTM scale 1-3.  The four per-pixel LSTMs are independent
+        of each other: lstm k forward runs beside the deeper encoder layers and lstm k
+        backward beside the remaining decoder backward, which leave most CUs idle at
+        1/16 and 1/32 resolution (lstm4 stays on the main stream: the decoder and the
+        encoder backward need it first).  3 side streams + main = GPU_MAX_HW_QUEUES."""
+        if self._side is None or self._side[0].device != dev:
+            self._side = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        return self._side
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
@@ -300,8 +311,13 @@ class STFProgram:
         S.pool_arg = torch.empty(N * h4 * w4 * 64, dtype=torch.uint8, device=dev) if training else None
         call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), _p(S.pool_arg), stream())
         S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
-        # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat)
+        # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat);
+        # lstm li (li < 3) starts on its side stream as soon as layer li is done
         S.enc, S.lbuf, S.pkbuf = [], [], []
+        side = self.side_streams(dev)
+        main = torch.cuda.current_stream(dev)
+        S.lstm = [None] * 4
+        dcat = [None] * 3          # decoder concat buffers (skip half = h_T of the LSTM one scale up)
         cur = p0
         for li, progs in enumerate(self.layers):
             C = progs[0].cout
@@ -327,29 +343,24 @@ class STFProgram:
             S.enc.append(saved)
             S.lbuf.append(lbuf)
             S.pkbuf.append(pkb)
-        # ---- decoder concat buffers (skip = h_T of the LSTM one scale up)
-        dcat = []
-        for d, lb in zip(self.decoders, (S.lbuf[2], S.lbuf[1], S.lbuf[0])):
-            Cout = d.up.out_channels
-            Cskip = d.fusion.in_channels - Cout
-            dcat.append(new_feat(B, lb.H, lb.W, Cout + Cskip, dev))
-        S.dcat = dcat
-        # ---- per-pixel LSTMs over T
-        S.lstm = []
-        e4f = None
-        for k, lp in enumerate(self.lstm_progs):
-            lb = S.lbuf[k]
-            if k < 3:
-                dc = dcat[2 - k]
-                hT = dc.slice(dc.C - lp.C, lp.C)
+            # ---- per-pixel LSTM of this scale over T
+            lp = self.lstm_progs[li]
+            if li < 3:
+                d = self.decoders[2 - li]
+                Cout = d.up.out_channels
+                dc = dcat[2 - li] = new_feat(B, hh, ww, Cout + d.fusion.in_channels - Cout, dev)
+                side[li].wait_stream(main)
+                with torch.cuda.stream(side[li]):
+                    S.lstm[li] = lp.forward(lbuf, T, B, dc.slice(dc.C - lp.C, lp.C))
             else:
-                e4f = new_feat(B, lb.H, lb.W, lp.C, dev)
-                hT = e4f
-            S.lstm.append(lp.forward(lb, T, B, hT))
+                e4f = new_feat(B, hh, ww, lp.C, dev)
+                S.lstm[li] = lp.forward(lbuf, T, B, e4f)
+        S.dcat = dcat
         # ---- decoder
         S.dec = []
         cur = e4f
         for i, d in enumerate(self.decoders):
+            main.wait_stream(side[2 - i])      # h_T of lstm 2-i fills the skip half of dcat[i]
             cat = dcat[i]
             Cout = d.up.out_channels
             nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, cat.slice(0, Cout), 3, 3, 2, 1,
@@ -408,8 +419,16 @@ class STFProgram:
         nhwc.igemm(d_u1, nhwc.pack_weight(up.weight, 3), S.d2out.C, dcur, 3, 3, 2, 1)
         del d_u1
         self._done(up)
-        # decoders 2, 3, 4 (reverse of forward order)
+        # decoders 2, 3, 4 (reverse of forward order); lstm k's backward starts on its
+        # side stream as soon as its h_T gradient (the decoder's skip slice) is final
+        side = self.side_streams(dev)
+        main = torch.cuda.current_stream(dev)
         dhT = [None] * 4
+        de = [None] * 4
+
+        def lstm_bwd(k):
+            de[k] = self.lstm_progs[k].backward(S.lstm[k], dhT[k], gv)
+            de[k].buf.record_stream(main)
         for i in (2, 1, 0):
             d, dsv = self.decoders[i], S.dec[i]
             Cout = d.up.out_channels
@@ -424,14 +443,22 @@ class STFProgram:
             nhwc.channel_sum(dup, gv(d.up.bias))
             dx = new_feat(B, dsv.x.H, dsv.x.W, dsv.x.C, dev)
             nhwc.igemm(dup, nhwc.pack_weight(d.up.weight, 3), dsv.x.C, dx, 3, 3, 2, 1)
-            dhT[2 - i] = dcat.slice(Cout, dcat.C - Cout)     # skip of scale 2-i (decoder4 -> scale 3 = idx 2)
+            k = 2 - i                                          # skip of scale k (decoder4 -> idx 2)
+            dhT[k] = dcat.slice(Cout, dcat.C - Cout)
+            side[k].wait_stream(main)
+            with torch.cuda.stream(side[k]):
+                lstm_bwd(k)
             dcur = dx
             self._done(d)
         dhT[3] = dcur                                          # decoder4 input = h_T of lstm4
-        # LSTMs (scale 4 first: its gradient is needed first by the encoder)
-        de = [None] * 4
+        lstm_bwd(3)
+        # join the side streams: all of them now when gradient buckets are being reduced
+        # (ready hooks must arrive in reverse flat order) or PK fusion needs every scale,
+        # else each just before the encoder layer that consumes its d x_t
+        eager = self.grad_ready_hook is not None or P
         for k in (3, 2, 1, 0):
-            de[k] = self.lstm_progs[k].backward(S.lstm[k], dhT[k], gv)
+            if eager and k < 3:
+                main.wait_stream(side[k])
             self._done(self.lstms[k])
         if P:
             for k in (3, 2, 1, 0):
@@ -440,6 +467,8 @@ class STFProgram:
         # encoder: layer4 -> layer1; d(layer k-1 output) accumulates into de[k-1]
         for li in (3, 2, 1, 0):
             progs, saved = self.layers[li], S.enc[li]
+            if li < 3:
+                main.wait_stream(side[li])
             dout = de[li]
             for bi in range(len(progs) - 1, -1, -1):
                 bp, s = progs[bi], saved[bi]

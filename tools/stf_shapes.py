@@ -11,26 +11,36 @@ from stfunet import nhwc, engine, STFLSTMUNet, UNet
 from stfunet.synthetic import dce_batch
 
 log = defaultdict(lambda: [0, 0.0])
+evs = defaultdict(list)
+TIME = False
 orig_igemm, orig_wgrad = nhwc.igemm, nhwc.wgrad
 
 
 def igemm(src, wgt, nout, dst, R, S, stride, pad, transposed=False, **kw):
+    e0 = torch.cuda.Event(enable_timing=True); e0.record()
     r = orig_igemm(src, wgt, nout, dst, R, S, stride, pad, transposed=transposed, **kw)
+    e1 = torch.cuda.Event(enable_timing=True); e1.record()
     Hd, Wd = (dst.H // 2, dst.W // 2) if kw.get("scatter2x2") else (dst.H, dst.W)
     fl = 2.0 * src.N * Hd * Wd * nout * R * S * src.C / (stride * stride if transposed else 1)
     key = (f"igemm {src.N}x{src.H}x{src.W}x{src.C} -> {Hd}x{Wd}x{nout} k{R}s{stride}"
            f"{' T' if transposed else ''}{' sc' if kw.get('scatter2x2') else ''}{' lstm' if kw.get('lstm') else ''}"
            f"{' bnr' if kw.get('bnr') else ''}")
-    log[key][0] += 1
-    log[key][1] += fl
+    if TIME:
+        log[key][0] += 1
+        log[key][1] += fl
+        evs[key].append((e0, e1))
     return r
 
 
 def wgrad(dy, x, R, S, stride, pad, out):
+    e0 = torch.cuda.Event(enable_timing=True); e0.record()
     r = orig_wgrad(dy, x, R, S, stride, pad, out)
+    e1 = torch.cuda.Event(enable_timing=True); e1.record()
     key = f"wgrad dy {dy.N}x{dy.H}x{dy.W}x{dy.C} x {x.H}x{x.W}x{x.C} k{R}s{stride}"
-    log[key][0] += 1
-    log[key][1] += 2.0 * dy.N * dy.H * dy.W * dy.C * R * S * x.C
+    if TIME:
+        log[key][0] += 1
+        log[key][1] += 2.0 * dy.N * dy.H * dy.W * dy.C * R * S * x.C
+        evs[key].append((e0, e1))
     return r
 
 
@@ -43,8 +53,16 @@ else:
 model.train()
 x, t = dce_batch(B, 8, 256, 256, seed=1, device=dev, mask_hw=half)
 x = engine.preprocess_input(x, model)
-loss = engine.criterion(model(x), t)
-loss.backward()
-torch.cuda.synchronize()
-for k, (n, fl) in sorted(log.items(), key=lambda kv: -kv[1][1]):
-    print(f"{n:3d} x {fl / n / 1e9:8.2f} GF  {k}")
+for it in range(3):
+    TIME = it == 2
+    for p in model.parameters():
+        p.grad = None
+    loss = engine.criterion(model(x), t)
+    loss.backward()
+    torch.cuda.synchronize()
+tot = 0.0
+for k, (n, fl) in sorted(log.items(), key=lambda kv: -sum(a.elapsed_time(b) for a, b in evs[kv[0]])):
+    ms = sum(a.elapsed_time(b) for a, b in evs[k])
+    tot += ms
+    print(f"{n:3d} x {fl / n / 1e9:8.2f} GF {ms / n * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s  {k}")
+print(f"total {tot:.3f} ms (each launch timed alone: events between launches)")
