@@ -263,6 +263,13 @@ int stf_pack_weights(const stf_pack_desc* descs, int count, int64_t max_elems, s
  * x[b][T+p][0] (src/stf_lstm_unet.py:146-156,172-174), rest zero. */
 int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int T, int P,
                       int Cpad, void* out, stf_stream_t stream);
+
+/* Stem im2col (replaces the padded-channel input of the 7x7/s2 stem, reference
+ * src/stf_lstm_unet.py:108,177): x as for stf_pack_sequence -> bf16
+ * [T*B][Ho][Wo][Kpad], column k = ci*KS*KS + r*KS + s (PyTorch weight order),
+ * zero padded; the stem conv is then a 1x1 GEMM over Kpad >= (C+P)*KS*KS columns. */
+int stf_stem_im2col(const float* x, int B, int Ttot, int C, int H, int W, int T, int P, int KS,
+                    int stride, int pad, int Kpad, void* out, stf_stream_t stream);
 /* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16.
  * argmax (uint8 [N][Ho][Wo][C], NULL in eval) records each window's first maximum
  * (index dy*3+dx, torch's tie rule); backward gathers dout over the <= 4 windows

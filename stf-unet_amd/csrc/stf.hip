@@ -41,6 +41,40 @@ __global__ void pack_sequence_kernel(const float* __restrict__ x, int B, int Tto
   }
 }
 
+// Stem im2col: cols[(t*B + b)][oy][ox][k], k = ci*KS*KS + r*KS + s (the PyTorch
+// [Cout][Cin][KS][KS] weight order), value = input channel ci of frame t at
+// (oy*st - pad + r, ox*st - pad + s), zero outside the image and for k >= Cin*KS*KS.
+// Input channel ci < C is x[b][t][ci], C <= ci < C+P the PK map x[b][T+ci-C][0]
+// (same channel order as pack_sequence).  One thread = 8 consecutive columns.
+__global__ void stem_im2col_kernel(const float* __restrict__ x, int B, int Ttot, int C, int H, int W, int T, int P,
+                                   int KS, int st, int pad, int Ho, int Wo, int Kpad, uint16_t* __restrict__ out) {
+  const long HW = (long)H * W, Pix = (long)T * B * Ho * Wo;
+  const int CG = Kpad / 8, KK = KS * KS, Kreal = (C + P) * KK;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < Pix * CG; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long pix = u / CG;
+    const long img = pix / ((long)Ho * Wo);
+    const int rem = (int)(pix - img * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
+    const int t = (int)(img / B), b = (int)(img - (long)t * B);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = cg * 8 + j;
+      float val = 0.f;
+      if (k < Kreal) {
+        const int ci = k / KK, rs = k - ci * KK, r = rs / KS, s = rs - r * KS;
+        const int iy = oy * st - pad + r, ix = ox * st - pad + s;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+          const long plane = ci < C ? ((long)b * Ttot + t) * C + ci : ((long)b * Ttot + T + (ci - C)) * C;
+          val = x[plane * HW + (long)iy * W + ix];
+        }
+      }
+      v[j] = val;
+    }
+    *reinterpret_cast<uint4*>(out + pix * Kpad + cg * 8) = pack8(v);
+  }
+}
+
 // MaxPool2d(k=3, s=2, p=1); first maximum in row-major window order (torch CPU)
 __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int Ho, int Wo,
                                     uint16_t* __restrict__ out, uint8_t* __restrict__ argmax) {
@@ -205,6 +239,18 @@ extern "C" int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, 
   const long units = (long)T * B * H * W * (Cpad / 8);
   hipLaunchKernelGGL(pack_sequence_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream, x, B,
                      Ttot, C, H, W, T, P, Cpad, (uint16_t*)out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_stem_im2col(const float* x, int B, int Ttot, int C, int H, int W, int T, int P, int KS,
+                               int stride, int pad, int Kpad, void* out, stf_stream_t stream) {
+  if (Kpad % 8 || Kpad < (C + P) * KS * KS || Ttot < T + P || (P && C != 1) || KS < 1 || stride < 1 || pad < 0)
+    return STF_EINVAL;
+  const int Ho = (H + 2 * pad - KS) / stride + 1, Wo = (W + 2 * pad - KS) / stride + 1;
+  const long units = (long)T * B * Ho * Wo * (Kpad / 8);
+  hipLaunchKernelGGL(stem_im2col_kernel, dim3(grid_for(units, 16384)), dim3(NT), 0, (hipStream_t)stream, x, B, Ttot,
+                     C, H, W, T, P, KS, stride, pad, Ho, Wo, Kpad, (uint16_t*)out);
   STF_CHECK_LAUNCH();
   return 0;
 }

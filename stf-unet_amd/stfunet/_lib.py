@@ -78,6 +78,8 @@ _SIGS = {
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weights": (c_int, [P, c_int, c_int64, P]),
     "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_stem_im2col": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                                P]),
     "stf_maxpool3s2_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "stf_lstm_pack": (c_int, [P, P, P, P, c_int, P, P, P, P]),

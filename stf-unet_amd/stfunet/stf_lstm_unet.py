@@ -33,10 +33,6 @@ from .flat import FlatParams
 from .nhwc import BNState, Feat, _p, new_feat, rows, zeros_feat
 
 
-def _c8(c):
-    return (c + 7) // 8 * 8
-
-
 # ------------------------------------------------------------------ module tree
 class BasicBlock(nn.Module):
     """torchvision ResNet BasicBlock parameter container (names are the contract)."""
@@ -295,13 +291,18 @@ class STFProgram:
         S = _S()
         S.B, S.T, S.P, S.H, S.W = B, T, P, H, W
         N = T * B
-        cpad = _c8(Cf + P)
-        xin = new_feat(N, H, W, cpad, dev)
-        call("stf_pack_sequence", _p(x), B, Ttot, Cf, H, W, T, P, cpad, xin.ptr(), stream())
-        # ---- stem
+        # ---- stem: conv 7x7/s2 over (Cf + P) <= 4 input channels as a 1x1 GEMM over the
+        # im2col columns (49 (Cf+P) of them, padded): a per-tap gather would pad every tap
+        # to 8 channels (8x the MFMA work at Cf = 1) and its weight gradient re-reads dy
+        # once per 64 columns
         h2, w2 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        kreal = (Cf + P) * 49
+        kpad = 64 if kreal <= 64 else (kreal + 31) // 32 * 32
+        xin = new_feat(N, h2, w2, kpad, dev)
+        call("stf_stem_im2col", _p(x), B, Ttot, Cf, H, W, T, P, 7, 2, 3, kpad, xin.ptr(), stream())
         y0 = new_feat(N, h2, w2, 64, dev)
-        stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(m.conv1.weight, 0, cpad), 64, y0, 7, 7, 2, 3,
+        w1 = m.conv1.weight
+        stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, kpad), 64, y0, 1, 1, 1, 0,
                                   want_stats=training, groups=T)
         S.bn0 = nhwc.bn_finalize(stats, tiles, m.bn1, y0.M, training, T)
         a0 = new_feat(N, h2, w2, 64, dev)
@@ -482,13 +483,14 @@ class STFProgram:
         da0 = new_feat(S.a0.N, S.a0.H, S.a0.W, 64, dev)
         call("stf_maxpool3s2_bwd", _p(S.pool_arg), dout.ptr(), S.a0.N, S.a0.H, S.a0.W, 64, da0.ptr(), stream())
         dy0 = nhwc.bn_backward(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), dz=da0)
-        cin = m.conv1.in_channels
-        if S.xin.C == cin:
-            nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, gv(m.conv1.weight))
+        w1 = m.conv1.weight
+        kreal = w1[0].numel()
+        if S.xin.C == kreal:
+            nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, gv(w1))
         else:
-            tmp = torch.empty(64 * S.xin.C * 49, dtype=torch.float32, device=dev)
-            nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp)
-            gv(m.conv1.weight).copy_(tmp.view(64, S.xin.C, 7, 7)[:, :cin])
+            tmp = torch.empty(w1.shape[0] * S.xin.C, dtype=torch.float32, device=dev)
+            nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, tmp)
+            gv(w1).copy_(tmp.view(w1.shape[0], S.xin.C)[:, :kreal].view(w1.shape))
 
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
         fus = getattr(self.m, f"pk_fusion{k + 1}")

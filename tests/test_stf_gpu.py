@@ -205,6 +205,40 @@ def test_pack_sequence_and_pk_resize():
         assert rel(d[t, :, 64:67], ref) < 4e-3
 
 
+@pytest.mark.parametrize("P", [0, 3])
+def test_stem_im2col_gemm(P):
+    """Stem conv 7x7/s2/p3 (src/stf_lstm_unet.py:108,177) as im2col + 1x1 GEMM:
+    columns bit-exact vs F.unfold of the bf16-rounded input; conv output and
+    weight gradient vs torch fp32 on bf16-rounded operands (rel L2 <= 1e-2)."""
+    from stfunet import nhwc
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
+    B, T, H, W = 2, 3, 40, 48
+    cin = 1 + P
+    kreal = cin * 49
+    kpad = 64 if kreal <= 64 else (kreal + 31) // 32 * 32
+    x = torch.randn(B, T + P, 1, H, W, device=DEV)
+    ho, wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    cols = nhwc.new_feat(T * B, ho, wo, kpad, DEV)
+    call("stf_stem_im2col", _p(x), B, T + P, 1, H, W, T, P, 7, 2, 3, kpad, cols.ptr(), stream())
+    frames = torch.cat([torch.cat([x[:, t], x[:, T:, 0]], 1) for t in range(T)], 0)     # [T*B, cin, H, W]
+    ref = F.unfold(bfr(frames), 7, padding=3, stride=2)                                  # [T*B, cin*49, ho*wo]
+    got = cols.dense().flatten(2)
+    assert torch.equal(got[:, :kreal].float(), ref)
+    assert got[:, kreal:].abs().max().item() == 0
+    w = torch.randn(64, cin, 7, 7, device=DEV) * 0.05
+    y = nhwc.new_feat(T * B, ho, wo, 64, DEV)
+    nhwc.igemm(cols, nhwc.pack_weight(w.view(64, -1, 1, 1), 0, kpad), 64, y, 1, 1, 1, 0)
+    yr = F.conv2d(bfr(frames), bfr(w), stride=2, padding=3)
+    assert rel(y.dense(), yr) < 1e-2
+    dy = bfr(torch.randn_like(yr))
+    dw = torch.empty(64 * kpad, device=DEV)
+    nhwc.wgrad(feat_from(dy), cols, 1, 1, 1, 0, dw)
+    wr = bfr(w).requires_grad_(True)
+    F.conv2d(bfr(frames), wr, stride=2, padding=3).backward(dy)
+    assert rel(dw.view(64, kpad)[:, :kreal].view(64, cin, 7, 7), wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("pk", [False, True])
 def test_stf_model_vs_golden(pk):
     from oracle.init import canonical_state_dict
