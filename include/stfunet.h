@@ -156,6 +156,21 @@ int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64_t M,
                     const float* gamma, const float* beta, float momentum, float eps,
                     float* running_mean, float* running_var, float* mean, float* invstd,
                     float* scale, float* shift, stf_stream_t stream);
+/* Deferred running-statistics update of grouped BatchNorms (groups > 1): a
+ * stf_bn_finalize call with running_mean = running_var = NULL leaves every
+ * group's (mean, biased var) parked in row 0 of that group's stats slab; one
+ * stf_bn_running_batch launch then advances each BatchNorm's running stats
+ * group by group, in order (same arithmetic as the in-call update).  descs is a
+ * HOST array; the stats slabs must stay alive until the launch has run. */
+typedef struct stf_bn_run_desc {
+  const float* stats;          /* [groups][tiles][2][C], parked by stf_bn_finalize */
+  float* running_mean;
+  float* running_var;
+  int64_t Mg;                  /* rows per group */
+  int tiles, groups, C;
+  float momentum;
+} stf_bn_run_desc;
+int stf_bn_running_batch(const stf_bn_run_desc* descs, int count, stf_stream_t stream);
 /* out = act(y*scale + shift [+ res | + res*res_scale + res_shift]) into a
  * channel slice.  Residual: identity shortcut (res_scale NULL) or a BN'd
  * downsample branch (ResNet BasicBlock src/stf_lstm_unet.py:108-114,
@@ -182,6 +197,17 @@ int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpool, const v
 int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C, int64_t M,
                         const float* gamma, const float* mean, const float* invstd,
                         float* dgamma, float* dbeta, float* coef, stf_stream_t stream);
+/* Deferred dgamma/dbeta of grouped BatchNorm backwards: stf_bn_bwd_finalize with
+ * dgamma = dbeta = NULL and groups > 1 leaves each group's (sum g, sum g*xhat)
+ * parked in row 0 of that group's partial slab; stf_bn_groupsum_batch sums them
+ * over the groups for many BatchNorms in one launch (descs: HOST array). */
+typedef struct stf_bn_gsum_desc {
+  const float* partial;        /* [groups][tiles][2][C] */
+  float* dgamma;
+  float* dbeta;
+  int tiles, groups, C;
+} stf_bn_gsum_desc;
+int stf_bn_groupsum_batch(const stf_bn_gsum_desc* descs, int count, stf_stream_t stream);
 /* dy = A*g' + B*y + C (bf16, dy_cstride; may alias g when dense).  g' = g, or
  * with mask_scale/mask_shift ([groups][C], the forward BN affine) the ReLU mask
  * recomputed from y: g' = g where y*scale+shift > 0 else 0 -- then g is the raw

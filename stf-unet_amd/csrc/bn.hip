@@ -74,12 +74,13 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(float* __restrict__ st
   invstd[g * C + c] = inv;
   scale[g * C + c] = sc;
   shift[g * C + c] = beta[c] - (float)mu * sc;
-  if (!(rm && stats)) return;
+  if (!stats) return;
   if (G == 1) {
+    if (!rm) return;
     const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
     rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
     rv[c] = (1.f - mom) * rv[c] + mom * (float)unb;
-  } else {
+  } else {                               // parked for bn_running_kernel / stf_bn_running_batch
     base[c] = (float)mu;
     base[C + c] = (float)var;
   }
@@ -302,6 +303,43 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* __restrict_
   }
 }
 
+// Deferred running-statistics updates of many grouped BatchNorms in one launch
+// (blockIdx.y = descriptor; same arithmetic as bn_running_kernel).
+constexpr int RUN_BATCH = 32;
+struct RunBatch { stf_bn_run_desc d[RUN_BATCH]; };
+__global__ void bn_running_batch_kernel(RunBatch b) {
+  const stf_bn_run_desc& d = b.d[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.C) return;
+  float run_m = d.running_mean[c], run_v = d.running_var[c];
+  const long Mg = (long)d.Mg;
+  for (int g = 0; g < d.groups; ++g) {
+    const float* base = d.stats + (size_t)g * d.tiles * 2 * d.C;
+    const double var = base[d.C + c];
+    const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
+    run_m = (1.f - d.momentum) * run_m + d.momentum * base[c];
+    run_v = (1.f - d.momentum) * run_v + d.momentum * (float)unb;
+  }
+  d.running_mean[c] = run_m;
+  d.running_var[c] = run_v;
+}
+
+// Deferred dgamma/dbeta sums of many grouped BatchNorm backwards in one launch
+struct GsumBatch { stf_bn_gsum_desc d[RUN_BATCH]; };
+__global__ void bn_groupsum_batch_kernel(GsumBatch b) {
+  const stf_bn_gsum_desc& d = b.d[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.C) return;
+  double dg = 0.0, db = 0.0;
+  for (int g = 0; g < d.groups; ++g) {
+    const float* base = d.partial + (size_t)g * d.tiles * 2 * d.C;
+    db += base[c];
+    dg += base[d.C + c];
+  }
+  if (d.dgamma) d.dgamma[c] = (float)dg;
+  if (d.dbeta) d.dbeta[c] = (float)db;
+}
+
 __global__ void bn_bwd_groupsum_kernel(const float* __restrict__ partial, int T, int G, int C, float* dgamma,
                                        float* dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -471,6 +509,36 @@ extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C,
   if (groups > 1 && (dgamma || dbeta)) {
     hipLaunchKernelGGL(bn_bwd_groupsum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, tiles, groups, C,
                        dgamma, dbeta);
+    STF_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int stf_bn_running_batch(const stf_bn_run_desc* descs, int count, stf_stream_t stream) {
+  for (int i = 0; i < count; ++i)
+    if (!descs[i].stats || !descs[i].running_mean || !descs[i].running_var || descs[i].groups < 1 ||
+        descs[i].C < 1 || descs[i].tiles < 1)
+      return STF_EINVAL;
+  for (int i0 = 0; i0 < count; i0 += RUN_BATCH) {
+    const int n = count - i0 < RUN_BATCH ? count - i0 : RUN_BATCH;
+    RunBatch b;
+    int cmax = 0;
+    for (int i = 0; i < n; ++i) { b.d[i] = descs[i0 + i]; cmax = cmax > b.d[i].C ? cmax : b.d[i].C; }
+    hipLaunchKernelGGL(bn_running_batch_kernel, dim3((cmax + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, b);
+    STF_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int stf_bn_groupsum_batch(const stf_bn_gsum_desc* descs, int count, stf_stream_t stream) {
+  for (int i = 0; i < count; ++i)
+    if (!descs[i].partial || descs[i].groups < 1 || descs[i].C < 1 || descs[i].tiles < 1) return STF_EINVAL;
+  for (int i0 = 0; i0 < count; i0 += RUN_BATCH) {
+    const int n = count - i0 < RUN_BATCH ? count - i0 : RUN_BATCH;
+    GsumBatch b;
+    int cmax = 0;
+    for (int i = 0; i < n; ++i) { b.d[i] = descs[i0 + i]; cmax = cmax > b.d[i].C ? cmax : b.d[i].C; }
+    hipLaunchKernelGGL(bn_groupsum_batch_kernel, dim3((cmax + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, b);
     STF_CHECK_LAUNCH();
   }
   return 0;

@@ -58,6 +58,8 @@ _SIGS = {
     "stf_wgrad_reduce": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_channel_sum": (c_int, [P, c_int, c_int, c_int, P, P, P]),
     "stf_bn_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, c_float, c_float, P, P, P, P, P, P, P]),
+    "stf_bn_running_batch": (c_int, [P, c_int, P]),
+    "stf_bn_groupsum_batch": (c_int, [P, c_int, P]),
     "stf_bn_act": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P, P, P, c_int, P,
                            P]),
     "stf_bn_bwd_tiles": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),

@@ -379,12 +379,40 @@ class BNState:
 # num_batches_tracked increments are deferred and applied per forward with one
 # multi-tensor launch per increment value (instead of one tiny kernel per module)
 _NBT_PENDING = {}
+_RUN_PENDING = []      # (stf_bn_run_desc, stats slab kept alive until the flush)
+_GSUM_PENDING = []     # (stf_bn_gsum_desc, partial slab)
+
+
+class _RunDesc(ctypes.Structure):
+    _fields_ = [("stats", ctypes.c_void_p), ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("Mg", ctypes.c_int64), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
+                ("momentum", ctypes.c_float)]
+
+
+class _GsumDesc(ctypes.Structure):
+    _fields_ = [("partial", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int)]
 
 
 def flush_batches_tracked():
+    """End of a training forward: the deferred running-statistics updates of the
+    grouped BatchNorms (one stf_bn_running_batch launch) and num_batches_tracked."""
+    if _RUN_PENDING:
+        arr = (_RunDesc * len(_RUN_PENDING))(*[d for d, _ in _RUN_PENDING])
+        call("stf_bn_running_batch", arr, len(_RUN_PENDING), stream())
+        _RUN_PENDING.clear()
     for inc, ts in _NBT_PENDING.items():
         torch._foreach_add_(ts, inc)
     _NBT_PENDING.clear()
+
+
+def flush_bn_grads():
+    """dgamma/dbeta of the grouped BatchNorm backwards run so far (one
+    stf_bn_groupsum_batch launch); call before those gradients are read."""
+    if _GSUM_PENDING:
+        arr = (_GsumDesc * len(_GSUM_PENDING))(*[d for d, _ in _GSUM_PENDING])
+        call("stf_bn_groupsum_batch", arr, len(_GSUM_PENDING), stream())
+        _GSUM_PENDING.clear()
 
 
 def bn_finalize(stats, tiles, bn, M, training, groups=1):
@@ -395,6 +423,12 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
     mom = 0.1 if bn.momentum is None else bn.momentum
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
+    if training and groups > 1 and rm is not None:
+        # grouped: (mean, var) of every group stay parked in the slab; the running
+        # stats advance group by group in ONE batched launch at the end of forward
+        _RUN_PENDING.append((_RunDesc(stats.data_ptr(), rm.data_ptr(), rv.data_ptr(), M // groups, tiles, groups, C,
+                                      float(mom)), stats))
+        rm = rv = None
     call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, _p(bn.weight.detach()),
          _p(bn.bias.detach()), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
          _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
@@ -486,6 +520,12 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
     dev = y.buf.device
     G = st.groups
     coef = torch.empty(G * 3 * C, dtype=torch.float32, device=dev)
+    if G > 1 and (dgamma is not None or dbeta is not None):
+        # grouped: the per-group sums stay parked; flush_bn_grads() adds them up for
+        # every pending BatchNorm in one launch
+        _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                                        dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
+        dgamma = dbeta = None
     call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, _p(bn.weight.detach()), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     bpart = None

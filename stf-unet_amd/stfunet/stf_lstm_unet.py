@@ -258,6 +258,7 @@ class STFProgram:
         return self._side
 
     def _done(self, module):
+        nhwc.flush_bn_grads()          # grouped BN dgamma/dbeta before the buckets read them
         if self.grad_ready_hook is not None:
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
@@ -277,6 +278,7 @@ class STFProgram:
         try:
             return self._backward(S, dlogits)
         finally:
+            nhwc.flush_bn_grads()
             nhwc.ACTIVE_PACKS = None
 
     def _forward(self, x, training, need_bwd):

@@ -92,6 +92,7 @@ def test_basic_block_grouped_bn(cin, cout, stride, groups):
     nhwc.flush_batches_tracked()                     # what the model programs do after forward
     gv = _Grads(blk)
     dsrc = prog.backward(s, gv, dout=feat_from(R))
+    nhwc.flush_bn_grads()                            # grouped dgamma/dbeta, as the programs do
     # torch reference: one BN batch per group, running stats advanced per group in order
     xr = x.clone().requires_grad_(True)
     outs = []
