@@ -93,7 +93,14 @@ typedef struct stf_igemm_args {
   const stf_lstm_epi* lstm; /* non-NULL: LSTM cell epilogue, dst unused          */
   const stf_bnr_epi* bnr;   /* non-NULL: fused BN-backward reduction (no stats,  */
                             /* no scatter/LSTM); group_rows = the BN's groups    */
+  float* ws;           /* split-K fp32 workspace of stf_igemm_ws_bytes(a) bytes */
+                       /* (16-B aligned), or NULL when that is 0 (ABI v4)      */
 } stf_igemm_args;
+
+/* Workspace bytes stf_igemm needs for these args: > 0 when the GEMM is split over
+ * K (small-M layers that would under-fill the chip; the partials are folded by a
+ * second launch that also writes the statistics). */
+size_t stf_igemm_ws_bytes(const stf_igemm_args* a);
 
 /* Partial-statistics rows per group for these args (the tiling depends on the
  * kernel chosen): size `stats` as groups * stf_igemm_stat_tiles(a) * 2 * Nout. */

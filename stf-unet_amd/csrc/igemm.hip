@@ -35,6 +35,9 @@ struct Geo {
   int bnr_relu; float* bnr_part;
   // stride-2 transposed gather with rows ordered by output parity class (see igemm_dma_kernel)
   int par;
+  // split-K (plain DMA kernels): blockIdx.z = K slice, fp32 partials [ksplit][M][Nout] in ws,
+  // folded by splitk_reduce_kernel (bias, bf16 store, BN statistics)
+  int ksplit; float* ws;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -493,9 +496,17 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   }
   constexpr uint32_t BAD = 0xFFFFFFF0u;
   const int tstep = (TRANS && a.par) ? 2 : 1;          // tap stride of the cursor
-  const int KT = C8 ? (a.K + BKK - 1) / BKK
-                    : ((TRANS && a.par) ? ((a.R - r0 + 1) >> 1) * ((a.S - s0 + 1) >> 1) * (a.Cs / BKK) : a.K / BKK);
+  const int KTall = C8 ? (a.K + BKK - 1) / BKK
+                       : ((TRANS && a.par) ? ((a.R - r0 + 1) >> 1) * ((a.S - s0 + 1) >> 1) * (a.Cs / BKK) : a.K / BKK);
   int tr = r0, ts = s0, tc = 0;                         // tap / channel cursor of the next K step to issue
+  // split-K (plain gathers only, see ksplit_of): this block's slice of the K steps
+  int KT = KTall;
+  if (!C8 && !TRANS && !SCATTER && EPI == 0 && a.ksplit > 1) {
+    const int kb = (int)((long)KTall * blockIdx.z / a.ksplit);
+    KT = (int)((long)KTall * (blockIdx.z + 1) / a.ksplit) - kb;
+    const int k0 = kb * BKK, tap = k0 / a.Cs;
+    tc = k0 - tap * a.Cs; tr = tap / a.S; ts = tap - tr * a.S;
+  }
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE;
@@ -579,6 +590,25 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (!C8 && !TRANS && !SCATTER && EPI == 0) {
+    if (a.ksplit > 1) {
+      // raw fp32 partial of this K slice: lane holds 4 consecutive channels of one row
+      float* wz = a.ws + (size_t)blockIdx.z * a.M * a.Nout;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WTM + i * 16 + fr;
+        if (m >= m_end) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WTN + j * 16 + fk * 4;
+          if (n < a.Nout)
+            *reinterpret_cast<float4*>(wz + (size_t)m * a.Nout + n) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+      return;
+    }
+  }
   __syncthreads();
   if constexpr (EPI == 0) {
     staged_epilogue<BM, BN, WM, WN, SCATTER, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx, pcls);
@@ -593,6 +623,70 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   }
 }
 
+
+// Split-K fold: dst = bf16(sum_z ws[z] + bias) (+ old dst), plus the BN partial
+// statistics of the stored values per row tile (tiles aligned to the statistic
+// groups: [G][tpg][2][Nout]).  Thread = 8 consecutive channels of SK_PASS rows
+// (a tile = SK_PASS * 256 / (Nout / 8) rows); every slab's loads for the SK_PASS
+// rows are issued together (the fold is latency-bound otherwise).
+constexpr int SK_PASS = 4;
+__host__ __device__ inline int sk_rows(int Nout) { return SK_PASS * (NT / (Nout / 8)); }
+__global__ __launch_bounds__(NT) void splitk_reduce_kernel(Geo a, int tpg) {
+  __shared__ float red[NT][17];
+  const int CG = a.Nout / 8, RPP = NT / CG, RB = SK_PASS * RPP;
+  const int grp = blockIdx.x / tpg, t = blockIdx.x - grp * tpg;
+  const int r0 = grp * a.Mg + t * RB, r1 = min(r0 + RB, (grp + 1) * a.Mg);
+  const int cg = threadIdx.x % CG, n = cg * 8, rr = threadIdx.x / CG;
+  float f[SK_PASS][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float bv = a.bias ? a.bias[n + e] : 0.f;
+#pragma unroll
+    for (int p = 0; p < SK_PASS; ++p) f[p][e] = bv;
+  }
+  const size_t slab = (size_t)a.M * a.Nout;
+  for (int z = 0; z < a.ksplit; ++z) {
+#pragma unroll
+    for (int p = 0; p < SK_PASS; ++p) {
+      const int m = r0 + rr + p * RPP;
+      if (m >= r1) continue;
+      const float* w = a.ws + z * slab + (size_t)m * a.Nout + n;
+      const float4 lo = *reinterpret_cast<const float4*>(w);
+      const float4 hi = *reinterpret_cast<const float4*>(w + 4);
+      f[p][0] += lo.x; f[p][1] += lo.y; f[p][2] += lo.z; f[p][3] += lo.w;
+      f[p][4] += hi.x; f[p][5] += hi.y; f[p][6] += hi.z; f[p][7] += hi.w;
+    }
+  }
+  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int p = 0; p < SK_PASS; ++p) {
+    const int m = r0 + rr + p * RPP;
+    if (m >= r1) continue;
+    uint16_t* d = a.dst + (size_t)m * a.dcs + n;
+    if (a.accumulate) {
+      float o[8];
+      unpack8(*reinterpret_cast<const uint4*>(d), o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[p][e] = round_bf(f[p][e]) + o[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[p][e] = round_bf(f[p][e]);
+    *reinterpret_cast<uint4*>(d) = pack8(f[p]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] += f[p][e]; s2[e] += f[p][e] * f[p][e]; }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[threadIdx.x][e] = s1[e]; red[threadIdx.x][8 + e] = s2[e]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.Nout; c += NT) {
+    const int g8 = c / 8, e = c - g8 * 8;
+    float u = 0.f, v = 0.f;
+    for (int q = g8; q < NT; q += CG) { u += red[q][e]; v += red[q][8 + e]; }
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + c] = u;
+    a.stats[(size_t)blockIdx.x * 2 * a.Nout + a.Nout + c] = v;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Halo kernel: 3x3 / stride 1 / pad 1 convolution (forward, and the stride-1
@@ -1233,7 +1327,7 @@ Cfg cfg_of(char k) {
 
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
 void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, bool c8, uint32_t src_bytes, hipStream_t s) {
-  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN, g.ksplit), block(64 * WM * WN);
 #define STF_D(TR, SCA, E) \
   hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, TR, SCA, E>), grid, block, 0, s, g, src_bytes)
   if (c8)
@@ -1249,7 +1343,7 @@ void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, bool c8, uint
 // plain forward gather (or its ConvT 2x2 scatter epilogue) on the 8-wave tiles
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
 void launch_dma_plain(const Geo& g, bool scatter, uint32_t src_bytes, hipStream_t s) {
-  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(64 * WM * WN);
+  dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN, g.ksplit), block(64 * WM * WN);
   if (scatter)
     hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, true, 0>), grid, block, 0, s, g,
                        src_bytes);
@@ -1297,12 +1391,36 @@ int halo_grid(const stf_igemm_args* a) {
   return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 ? 2 : 1));
 }
 
+// Split-K factor for a plain gather on the linear DMA kernels that would leave the
+// chip under-filled (small-M layers: STF layer4 at 8x8, LSTM backward GEMMs):
+// K slices until ~256 workgroups, each keeping >= 8 K steps.  1 = no split.
+// STF_SPLITK=0 disables it (A/B).
+int ksplit_of(const stf_igemm_args* a) {
+  static const bool on = [] { const char* e = getenv("STF_SPLITK"); return !(e && e[0] == '0'); }();
+  const stf_conv_geom& c = a->g;
+  const char k = choose(a, dma_fits(a));
+  if (!on || a->lstm || a->scatter2x2 || c.transposed || c.Cs == 8) return 1;
+  if (!(k == 'A' || k == 'B' || k == 'C' || k == 'D' || k == 'E')) return 1;
+  if (a->Nout % 8 || NT % (a->Nout / 8) || a->dst_cstride % 8 || ((uintptr_t)a->dst & 15)) return 1;
+  const Cfg f = cfg_of(k);
+  const long M = (long)c.N * c.Hd * c.Wd;
+  const long Mg = a->group_rows > 0 ? a->group_rows : M;
+  const long blocks = (M / Mg) * ((Mg + f.bm - 1) / f.bm) * ((a->Nout + f.bn - 1) / f.bn);
+  const long kt = (long)c.R * c.S * c.Cs / f.bkk;
+  if (blocks >= 192 || kt < 16) return 1;
+  long ks = (256 + blocks - 1) / blocks;
+  if (ks > kt / 8) ks = kt / 8;
+  if (ks > 8) ks = 8;
+  return ks < 2 ? 1 : (int)ks;
+}
+
 // BatchNorm partial-statistics rows per group for the kernel that will run
 int stat_tiles(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
   if (choose(a, dma_fits(a)) == 'H') return halo_grid(a);
+  if (ksplit_of(a) > 1) return (int)((Mg + sk_rows(a->Nout) - 1) / sk_rows(a->Nout));
   const int bm = pick_mtile(a);
   return (int)((Mg + bm - 1) / bm);
 }
@@ -1310,6 +1428,13 @@ int stat_tiles(const stf_igemm_args* a) {
 }  // namespace
 
 extern "C" int stf_igemm_stat_tiles(const stf_igemm_args* a) { return stat_tiles(a); }
+
+extern "C" size_t stf_igemm_ws_bytes(const stf_igemm_args* a) {
+  const int ks = ksplit_of(a);
+  if (ks < 2) return 0;
+  const stf_conv_geom& c = a->g;
+  return (size_t)ks * c.N * c.Hd * c.Wd * a->Nout * sizeof(float);
+}
 
 extern "C" int stf_igemm_bnr_tiles(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
@@ -1390,6 +1515,7 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.bnr_y = nullptr; g.bnr_ycs = 0; g.bnr_scale = g.bnr_shift = g.bnr_mean = g.bnr_invstd = nullptr;
   g.bnr_relu = 0; g.bnr_part = nullptr;
   g.par = 0;
+  g.ksplit = 1; g.ws = nullptr;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
@@ -1459,6 +1585,11 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     g.par = 1;
     g.tpg = (int)blocks;
   }
+  const int ks = ksplit_of(a);
+  if (ks > 1) {
+    if (!a->ws || ((uintptr_t)a->ws & 15)) return STF_EINVAL;
+    g.ksplit = ks; g.ws = a->ws;
+  }
   switch (k) {
     case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
     case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
@@ -1472,5 +1603,10 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
       return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
   }
   STF_CHECK_LAUNCH();
+  if (g.ksplit > 1) {
+    const int tpg = (g.Mg + sk_rows(g.Nout) - 1) / sk_rows(g.Nout);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(tpg * (g.M / g.Mg)), dim3(NT), 0, s, g, tpg);
+    STF_CHECK_LAUNCH();
+  }
   return 0;
 }

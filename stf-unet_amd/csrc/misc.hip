@@ -203,4 +203,4 @@ extern "C" const char* stf_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-extern "C" int stf_abi_version(void) { return 3; }
+extern "C" int stf_abi_version(void) { return 4; }

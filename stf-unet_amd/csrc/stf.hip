@@ -46,10 +46,12 @@ __global__ void pack_sequence_kernel(const float* __restrict__ x, int B, int Tto
 // (oy*st - pad + r, ox*st - pad + s), zero outside the image and for k >= Cin*KS*KS.
 // Input channel ci < C is x[b][t][ci], C <= ci < C+P the PK map x[b][T+ci-C][0]
 // (same channel order as pack_sequence).  One thread = 8 consecutive columns.
+template <int KS>
 __global__ void stem_im2col_kernel(const float* __restrict__ x, int B, int Ttot, int C, int H, int W, int T, int P,
-                                   int KS, int st, int pad, int Ho, int Wo, int Kpad, uint16_t* __restrict__ out) {
+                                   int st, int pad, int Ho, int Wo, int Kpad, uint16_t* __restrict__ out) {
   const long HW = (long)H * W, Pix = (long)T * B * Ho * Wo;
-  const int CG = Kpad / 8, KK = KS * KS, Kreal = (C + P) * KK;
+  constexpr int KK = KS * KS;            // compile-time: the column -> (ci, r, s) split is multiplies
+  const int CG = Kpad / 8, Kreal = (C + P) * KK;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < Pix * CG; u += (long)gridDim.x * NT) {
     const int cg = (int)(u % CG);
     const long pix = u / CG;
@@ -249,8 +251,9 @@ extern "C" int stf_stem_im2col(const float* x, int B, int Ttot, int C, int H, in
     return STF_EINVAL;
   const int Ho = (H + 2 * pad - KS) / stride + 1, Wo = (W + 2 * pad - KS) / stride + 1;
   const long units = (long)T * B * Ho * Wo * (Kpad / 8);
-  hipLaunchKernelGGL(stem_im2col_kernel, dim3(grid_for(units, 16384)), dim3(NT), 0, (hipStream_t)stream, x, B, Ttot,
-                     C, H, W, T, P, KS, stride, pad, Ho, Wo, Kpad, (uint16_t*)out);
+  if (KS != 7) return STF_EINVAL;         // the ResNet stem (other sizes: add an instantiation)
+  hipLaunchKernelGGL(stem_im2col_kernel<7>, dim3(grid_for(units, 16384)), dim3(NT), 0, (hipStream_t)stream, x, B,
+                     Ttot, C, H, W, T, P, stride, pad, Ho, Wo, Kpad, (uint16_t*)out);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -38,7 +38,7 @@ class IgemmArgs(ctypes.Structure):
     _fields_ = [("g", ConvGeom), ("src", P), ("wgt", P), ("Nout", c_int), ("dst", P),
                 ("dst_cstride", c_int), ("bias", P), ("stats", P), ("scatter2x2", c_int),
                 ("group_rows", c_int), ("accumulate", c_int), ("lstm", ctypes.POINTER(LstmEpi)),
-                ("bnr", ctypes.POINTER(BnrEpi))]
+                ("bnr", ctypes.POINTER(BnrEpi)), ("ws", P)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -49,6 +49,7 @@ class WgradArgs(ctypes.Structure):
 # name -> (restype, argtypes)
 _SIGS = {
     "stf_igemm_stat_tiles": (c_int, [ctypes.POINTER(IgemmArgs)]),
+    "stf_igemm_ws_bytes": (c_size_t, [ctypes.POINTER(IgemmArgs)]),
     "stf_igemm_bnr_tiles": (c_int, [ctypes.POINTER(IgemmArgs)]),
     "stf_igemm_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(IgemmArgs)]),
     "stf_wgrad_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(WgradArgs)]),

@@ -296,6 +296,11 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
                                                       bnr is not None, want_stats), a)
         if not t.wants(name):
             t = None
+    ws = None
+    nb = _lib.load().stf_igemm_ws_bytes(ctypes.byref(a))
+    if nb:
+        ws = torch.empty(nb // 4, dtype=torch.float32, device=dst.buf.device)
+        a.ws = _p(ws)
     ev = t.begin() if t is not None else None
     call("stf_igemm", ctypes.byref(a), stream())
     if t is not None:

@@ -172,6 +172,40 @@ def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     assert rel(dx.dense(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W,R,groups,acc", [
+    (16, 512, 512, 8, 8, 3, 8, False),           # STF layer4 shape (per-time-step groups), split 8
+    (4, 2048, 1024, 8, 8, 1, 1, False),          # LSTM-backward-like 1x1, split 4
+    (8, 256, 256, 8, 12, 3, 2, True),            # accumulate into dst, grouped
+])
+def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
+    """Small-M plain gathers run split over K (fp32 partials + fold launch): output,
+    accumulate, bias and grouped BN partial statistics vs torch fp32."""
+    import ctypes
+    from stfunet import _lib, nhwc
+    pad = R // 2
+    x = bfr(torch.randn(n, cin, H, W, device=DEV))
+    w = bfr(torch.randn(cout, cin, R, R, device=DEV) / (cin * R * R) ** 0.5)
+    b = torch.randn(cout, device=DEV)
+    ref = F.conv2d(x, w, b, padding=pad)
+    dst = nhwc.new_feat(n, H, W, cout, DEV)
+    if acc:
+        base = bfr(torch.randn_like(ref))
+        dst.buf.view(n, H, W, cout).copy_(base.permute(0, 2, 3, 1).to(torch.bfloat16))
+        ref = ref + base
+    src = feat_from(x)
+    a = _lib.IgemmArgs(nhwc._geom(src, H, W, R, R, 1, pad, False), src.ptr(), None, cout, dst.ptr(), cout)
+    assert _lib.load().stf_igemm_ws_bytes(ctypes.byref(a)) > 0, "shape expected to run split over K"
+    stats, tiles = nhwc.igemm(src, nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst, R, R, 1, pad, bias=b,
+                              want_stats=True, groups=groups, accumulate=acc)
+    out = dst.dense()
+    assert rel(out, ref) < 1e-2
+    st = stats.view(groups, tiles, 2, cout).sum(1)
+    og = out.view(groups, n // groups, cout, H, W)
+    for g in range(groups):
+        assert rel(st[g, 0], og[g].sum((0, 2, 3))) < 2e-3
+        assert rel(st[g, 1], (og[g] ** 2).sum((0, 2, 3))) < 2e-3
+
+
 @pytest.mark.parametrize("n,cin,cout,H,W,groups,relu,acc", [
     (2, 64, 128, 40, 72, 1, True, False),     # halo 16x32 tiles, ragged edges
     (4, 128, 64, 24, 20, 2, True, False),     # halo 16x16 tiles, two BN groups
