@@ -331,6 +331,30 @@ int stf_lstm_cell_bwd(const float* gates, const float* c_t, const float* c_prev,
 int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int H, int W, int h, int w,
                   void* dst, int dst_cstride, int coff, stf_stream_t stream);
 
+/* ---------------------------------------------------------------- PK maps (extended Tofts)
+ * pk_fitting.py ToftsModelFitter, all fp32.  The host builds
+ * the reference's constant tables exactly as the reference does (pk_fitting.py:
+ * 193-203): time_points t[T], cp_t = Cp(t), the convolution grid tau = arange(0,
+ * t[T-1], dt) and cp_tau = Cp(tau) (n_conv entries), and n_valid[i] = #{tau_j < t_i}
+ * (device int array).  T <= 32, n_conv <= 8192. */
+/* C[P][T] = extended_tofts_model_batch(t, ktrans, ve, vp) (pk_fitting.py:193-231). */
+int stf_tofts_forward(const float* ktrans, const float* ve, const float* vp, int P, int T,
+                      const float* time_points, const float* cp_t, const float* tau,
+                      const float* cp_tau, const int* n_valid, int n_conv, float dt, float* out,
+                      stf_stream_t stream);
+/* The fit loop of fit_volume_gpu (pk_fitting.py:280-365) for P tissue curves [P][T]
+ * (row-major pixel order): batches of `batch` pixels, `epochs` passes, torch Adam
+ * over the whole parameter vectors after every batch (pixels outside the batch take
+ * a zero-gradient step), clamps after each step.  params [3][P] (Ktrans, ve, vp):
+ * initial values in, fitted values out.  adam_sched: DEVICE [epochs*nbatches][2] =
+ * (lr / (1 - beta1^s), sqrt(1 - beta2^s)) for s = 1.. (double-precision bias
+ * corrections rounded to fp32, as torch applies them).  bounds: HOST [3][2] clamp
+ * ranges. */
+int stf_tofts_fit(const float* curves, int P, int T, const float* time_points, const float* cp_t,
+                  const float* tau, const float* cp_tau, const int* n_valid, int n_conv, float dt,
+                  int batch, int epochs, const float* adam_sched, float beta1, float beta2, float eps,
+                  const float* bounds, float* params, stf_stream_t stream);
+
 const char* stf_error_string(int code);
 int stf_abi_version(void);
 

@@ -166,3 +166,19 @@ def test_flop_count_matches_survey():
     # UNet 256^2 in=8 fwd 96.72 GFLOP/sample, 128^2 24.18
     assert abs(o_unet.train_flops_per_sample(8, 64, 256, 256) / 3 / 1e9 - 96.72) < 0.05
     assert abs(o_unet.train_flops_per_sample(8, 64, 128, 128) / 3 / 1e9 - 24.18) < 0.05
+
+
+def test_pk_tofts_oracle_vs_reference():
+    """oracle.pk (extended Tofts model + per-pixel Adam fit, pk_fitting.py:193-420)
+    against the reference's own outputs (tests/golden/make_golden_pk.py): the model
+    bit-exact, the 200-step fit within 1e-6 relative (analytic vs autograd gradients)."""
+    from oracle import pk as o_pk
+    g = np.load(os.path.join(GOLDEN, "pk_tofts.npz"))
+    out, _ = o_pk.tofts(g["time_points"], torch.from_numpy(g["fwd_ktrans"]), torch.from_numpy(g["fwd_ve"]),
+                        torch.from_numpy(g["fwd_vp"]))
+    assert torch.equal(out, torch.from_numpy(g["fwd_out"]))
+    maps = o_pk.fit_volume(g["images"], g["tissue"], torch.from_numpy(g["time_points"]))
+    ref = torch.from_numpy(g["param_maps"])
+    for k in range(3):
+        assert ((maps[k] - ref[k]).norm() / ref[k].norm()).item() < 1e-6
+        assert (maps[k] - ref[k]).abs().max().item() < 1e-6
