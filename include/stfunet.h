@@ -331,6 +331,16 @@ int stf_lstm_cell_bwd(const float* gates, const float* c_t, const float* c_prev,
 int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int H, int W, int h, int w,
                   void* dst, int dst_cstride, int coff, stf_stream_t stream);
 
+/* ---------------------------------------------------------------- evaluation
+ * One pass over a batch's logits [B][K][HW] (fp32, NCHW) and int64 targets [B][HW]
+ * (train_utils/train_and_eval.py:30-39, 80-118, 316-336): pred = first argmax over K;
+ * confmat [K][K] += (target t in [0,K)) at [t][pred]; dice_counts [K][3] += per-class
+ * (|P&T|, |P|, |T|) after multiplying pred and target by (target != ignore_index)
+ * when ignore_index >= 0 (the reference's DiceCoefficient masking).  Both outputs are
+ * int64 device arrays that ACCUMULATE (zero them first).  K <= 16. */
+int stf_eval_counts(const float* logits, const int64_t* target, int B, int K, int64_t HW,
+                    int64_t ignore_index, int64_t* confmat, int64_t* dice_counts, stf_stream_t stream);
+
 /* ---------------------------------------------------------------- PK maps (extended Tofts)
  * pk_fitting.py ToftsModelFitter, all fp32.  The host builds
  * the reference's constant tables exactly as the reference does (pk_fitting.py:

@@ -81,6 +81,7 @@ _SIGS = {
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weights": (c_int, [P, c_int, c_int64, P]),
     "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "stf_eval_counts": (c_int, [P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_tofts_forward": (c_int, [P, P, P, c_int, c_int, P, P, P, P, P, c_int, c_float, P, P]),
     "stf_tofts_fit": (c_int, [P, c_int, c_int, P, P, P, P, P, c_int, c_float, c_int, c_int, P, c_float, c_float,
                               c_float, P, P, P]),

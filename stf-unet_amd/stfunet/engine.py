@@ -239,6 +239,36 @@ class MetricLogger:
                                                          total / max(n, 1)))
 
 
+def eval_update(out, target, confmat, dice):
+    """One batch of evaluate(): ``confmat.update(target, argmax)`` + ``dice.update(out,
+    target)`` as ONE stf_eval_counts pass over the logits (argmax, confusion counts,
+    per-class Dice counts; no host synchronisation), then the per-batch Dice from the
+    counts exactly as DiceCoefficient.update computes it (train_and_eval.py:80-118)."""
+    from ._lib import call, stream
+    from .nhwc import _p
+    if not out.is_cuda:
+        raise RuntimeError("engine.evaluate runs the gfx950 stf_eval_counts kernel: logits must be on a ROCm "
+                           "device (no CPU fallback)")
+    out = out.detach().float().contiguous()
+    target = target.to(device=out.device, dtype=torch.int64).contiguous()
+    B, K = out.shape[:2]
+    if confmat.mat is None:
+        confmat.mat = torch.zeros((K, K), dtype=torch.int64, device=out.device)
+    counts = torch.zeros((K, 3), dtype=torch.int64, device=out.device)
+    ign = dice.ignore_index if dice.ignore_index is not None else -1
+    call("stf_eval_counts", _p(out), _p(target), B, K, out[0, 0].numel(), ign, _p(confmat.mat), _p(counts),
+         stream())
+    inter, psum, tsum = counts.float().unbind(1)
+    union = psum + tsum
+    d = torch.where(union > 0, 2.0 * inter / union.clamp_min(1.0), torch.ones_like(union))
+    if dice.cumulative_dice is None:
+        dice.cumulative_dice = d
+        dice.count = 1
+    else:
+        dice.cumulative_dice = dice.cumulative_dice + d
+        dice.count += 1
+
+
 def evaluate(model, data_loader, device, num_classes):
     model.eval()
     confmat = ConfusionMatrix(num_classes)
@@ -249,8 +279,7 @@ def evaluate(model, data_loader, device, num_classes):
             image = preprocess_input(image, model).to(device)
             target = target.to(device)
             out = model(image)["out"]
-            confmat.update(target.flatten(), out.argmax(1).flatten())
-            dice.update(out, target)
+            eval_update(out, target, confmat, dice)
         confmat.reduce_from_all_processes()
         dice.reduce_from_all_processes()
         mat = confmat.mat.cpu().numpy()
