@@ -64,6 +64,12 @@ class AdamW(torch.optim.Optimizer):
         self._flat[gi] = fb
         return fb
 
+    def load_state_dict(self, state_dict):
+        """Resume (train.py:249-256): torch rebuilds ``self.state`` with new tensors, so
+        the flat buffers are re-laid from them at the next step."""
+        super().load_state_dict(state_dict)
+        self._flat = {}
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None

@@ -199,3 +199,40 @@ def test_autocast_gradscaler_step():
     for k in p0:
         d = (p0[k] - p1[k]).abs().max().item()
         assert d <= 2.2 * 2e-3 + 1e-6, (k, d)
+
+
+def test_checkpoint_resume_bitwise():
+    """train.py:289-311 checkpoint dict {'model','optimizer','lr_scheduler','epoch','args'}
+    through torch.save / torch.load(weights_only=True), resumed into a FRESH model,
+    optimizer and scheduler (train.py:249-256): the next steps match an uninterrupted
+    run bit for bit (deterministic kernels, flat optimizer state re-laid on load)."""
+    import io
+    from stfunet import engine
+    from stfunet.optim import AdamW
+    batches = [dce_case(31 + i, 2, 8, 64, 64) for i in range(4)]
+
+    def make(seed):
+        model, _ = _model(8, seed=seed)
+        opt = AdamW(list(model.parameters()), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
+        return model, opt, engine.create_lr_scheduler(opt, 2, 3, warmup=True)
+
+    model, opt, sched = make(9)
+    engine.train_one_epoch(model, opt, batches[:2], torch.device(DEV), 0, 2, lr_scheduler=sched, print_freq=100)
+    buf = io.BytesIO()
+    torch.save({"model": model.state_dict(), "optimizer": opt.state_dict(), "lr_scheduler": sched.state_dict(),
+                "epoch": 0, "args": {"lr": 1e-3, "epochs": 3}}, buf)
+    engine.train_one_epoch(model, opt, batches[2:], torch.device(DEV), 1, 2, lr_scheduler=sched, print_freq=100)
+    want = {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+    buf.seek(0)
+    ck = torch.load(buf, weights_only=True, map_location=DEV)
+    model2, opt2, sched2 = make(123)                   # different init: everything must come from ck
+    model2.load_state_dict(ck["model"])
+    opt2.load_state_dict(ck["optimizer"])
+    sched2.load_state_dict(ck["lr_scheduler"])
+    engine.train_one_epoch(model2, opt2, batches[2:], torch.device(DEV), ck["epoch"] + 1, 2, lr_scheduler=sched2,
+                           print_freq=100)
+    got = model2.state_dict()
+    for k, v in want.items():
+        assert torch.equal(got[k], v), k
+    assert sched2.get_last_lr() == sched.get_last_lr()
