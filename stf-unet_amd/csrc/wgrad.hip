@@ -678,7 +678,8 @@ void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
   const int M = a->g.N * a->g.Hd * a->g.Wd;
   const int bm = big_tile(a) ? 128 : 64, bkp = big_tile(a) ? 32 : 64;
   const long rsc = (long)a->g.R * a->g.S * a->g.Cs;
-  const long tiles = (long)((a->Nout + bm - 1) / bm) * ((rsc + bm - 1) / bm);
+  const long cblocks = (a->g.Cs % 64 && rsc > 64 && rsc <= 96) ? 1 : (rsc + bm - 1) / bm;
+  const long tiles = (long)((a->Nout + bm - 1) / bm) * cblocks;
   long want = (2048 + tiles - 1) / tiles;
   long maxs = (M + 4 * bkp - 1) / (4 * bkp);        // at least 4 K steps per split
   if (want > maxs) want = maxs;
@@ -704,7 +705,9 @@ extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
   }
   if (const int pw = fused22_pw(a)) return pw == 16 ? "wgrad2x2s2_kernel<16>" : "wgrad2x2s2_kernel<8>";
   if (big_tile(a)) return "wgrad_kernel<128, 128, 32, false>";
-  return a->g.Cs % 64 == 0 ? "wgrad_kernel<64, 64, 64, false>" : "wgrad_kernel<64, 64, 64, true>";
+  const int rsc = a->g.R * a->g.S * a->g.Cs;
+  if (a->g.Cs % 64 == 0) return "wgrad_kernel<64, 64, 64, false>";
+  return (rsc > 64 && rsc <= 96) ? "wgrad_kernel<64, 96, 64, true>" : "wgrad_kernel<64, 64, 64, true>";
 }
 
 extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
@@ -753,6 +756,11 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   } else if (c.Cs % 64 == 0) {
     dim3 grid(splits, (a->Nout + 63) / 64, rsc / 64);
     hipLaunchKernelGGL((wgrad_kernel<64, 64, 64, false>), grid, dim3(NT), 0, s, w);
+  } else if (rsc > 64 && rsc <= 96) {
+    // 8-channel network input, 3x3 (72 columns): one 96-column block reads dy once
+    // (two 64-column blocks would read the 64-channel dy twice)
+    dim3 grid(splits, (a->Nout + 63) / 64, 1);
+    hipLaunchKernelGGL((wgrad_kernel<64, 96, 64, true>), grid, dim3(NT), 0, s, w);
   } else {
     dim3 grid(splits, (a->Nout + 63) / 64, (rsc + 63) / 64);
     hipLaunchKernelGGL((wgrad_kernel<64, 64, 64, true>), grid, dim3(NT), 0, s, w);
