@@ -4,6 +4,7 @@
 #   2. rocprofv3 --kernel-trace --stats of the SAME commands (per-kernel averages that
 #      the bench line's roofline avg_launch_us is checked against)
 #   3. the two PMC passes (HBM traffic, tools/pmc_passes.sh) per model -> pmc_traffic_*.json
+#   4. the PK-map fit bench (tools/bench_pk.py) under rocprofv3, the eval-metric micro-bench
 # Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
 set -e
 tag=${1:-r01}
@@ -17,7 +18,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/u
   python3 $root/bench.py > $out/unet_rocprof_bench.json 2> $out/unet.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stf -o run -- \
   python3 $root/bench.py --model stf > $out/stf_rocprof_bench.json 2> $out/stf.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pk -o run -- \
+  python3 $root/tools/bench_pk.py > $out/bench_pk.json 2> $out/pk.log
 cd $root
+timeout -k 10 200 python3 tools/bench_eval.py > $out/bench_eval.txt 2>&1
 if [ -z "$SKIP_PMC" ]; then
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_unet --steps 3 --warmup 1
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_stf --model stf --steps 3 --warmup 1
@@ -30,5 +34,6 @@ python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_stf --batch 16 \
 fi
 cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
 cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
-rm -rf $out/unet $out/stf $out/pmc_unet $out/pmc_stf
+cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
+rm -rf $out/unet $out/stf $out/pk $out/pmc_unet $out/pmc_stf
 ls $out
