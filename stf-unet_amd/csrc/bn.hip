@@ -271,6 +271,91 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
   }
 }
 
+// The pooled reduce with one lane per PIXEL (the 4 pixels of a 2x2 window in the 4
+// lanes of a DPP quad, 8 channels each): the window's first maximum of relu(BN(y))
+// (bf16-rounded, as the forward stored it) comes from two quad_perm DPP moves, so a
+// lane holds 3 loads and a few dozen registers instead of a whole window (13 loads,
+// ~150 registers: occupancy/latency bound at 3.4 TB/s).  Unit u: window pixel d =
+// u & 3, channel chunk (u >> 2) % CG, window (u >> 2) / CG.  Needs 64 % (C / 8) == 0
+// (the grid stride then keeps a thread's d and chunk fixed).
+STF_DEV float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));   // [1,0,3,2]
+}
+STF_DEV float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));   // [2,3,0,1]
+}
+
+constexpr int PNT = 512;                      // 2x the waves of the other BN kernels: more loads in flight
+__global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t* __restrict__ dz, int dzcs,
+                                          const uint16_t* __restrict__ dpool, const uint16_t* __restrict__ y,
+                                          int ycs, long N, int H, int W, int C, int G, int tpg,
+                                          const float* __restrict__ scale, const float* __restrict__ shift,
+                                          const float* __restrict__ mean, const float* __restrict__ invstd,
+                                          int mask_mode, uint16_t* __restrict__ g_out,
+                                          float* __restrict__ partial) {
+  __shared__ float red[PNT][17];
+  const int CG = C / 8;
+  const int g = blockIdx.x / tpg, tile = blockIdx.x - g * tpg;
+  const int Wp = W / 2, Hp = H / 2;
+  const long wpg = (N / G) * Hp * Wp;                       // windows per group
+  const long U = wpg * CG * 4;
+  const long gt = (long)tile * PNT + threadIdx.x;
+  const int d = (int)(gt & 3);
+  const int cg = (int)((gt >> 2) % CG);
+  float sc[8], sh[8], mu[8], is[8];
+  load_affine(scale + (size_t)g * C, cg * 8, sc);
+  load_affine(shift + (size_t)g * C, cg * 8, sh);
+  load_affine(mean + (size_t)g * C, cg * 8, mu);
+  load_affine(invstd + (size_t)g * C, cg * 8, is);
+  const bool relu = mask_mode == 1;
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // 32-bit index math (a 64-bit division is a long emulated sequence per unit): every
+  // tensor here has < 2^31 windows and pixels (checked by the host)
+  const int HpWp = Hp * Wp, cshift = __builtin_ctz(CG);   // CG is a power of two (64 % CG == 0)
+  for (long u = gt; u < U; u += (long)tpg * PNT) {
+    const int win = (int)(u >> (2 + cshift)) + (int)(g * wpg);
+    const int n = win / HpWp;
+    const int rem = win - n * HpWp;
+    const int py = rem / Wp, px = rem - py * Wp;
+    const long p = ((long)(n * H + 2 * py + (d >> 1))) * W + 2 * px + (d & 1);
+    float v[8], gd[8], dp[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + p * ycs + cg * 8), v);
+    if (dz) unpack8(*reinterpret_cast<const uint4*>(dz + p * dzcs + cg * 8), gd);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gd[j] = 0.f;
+    }
+    unpack8(*reinterpret_cast<const uint4*>(dpool + (long)win * C + cg * 8), dp);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = v[j] * sc[j] + sh[j];
+      const float a = round_bf(relu ? fmaxf(t, 0.f) : t);
+      float m = fmaxf(a, quad_xor1(a));
+      m = fmaxf(m, quad_xor2(m));
+      float c = a == m ? (float)d : 4.f;                       // first maximum of the window
+      c = fminf(c, quad_xor1(c));
+      c = fminf(c, quad_xor2(c));
+      float gj = gd[j] + (c == (float)d ? dp[j] : 0.f);
+      if (relu && !(t > 0.f)) gj = 0.f;
+      gd[j] = gj;
+      sg[j] += gj;
+      sgx[j] += gj * (v[j] - mu[j]) * is[j];
+    }
+    *reinterpret_cast<uint4*>(g_out + p * C + cg * 8) = pack8(gd);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += PNT) {
+    const int gg = c / 8, j = c - gg * 8;
+    float a = 0.f, b = 0.f;
+    for (int t = 4 * gg; t < PNT; t += 4 * CG)               // threads holding chunk gg: (t >> 2) % CG == gg
+      for (int q = 0; q < 4; ++q) { a += red[t + q][j]; b += red[t + q][8 + j]; }
+    partial[(size_t)blockIdx.x * 2 * C + c] = a;
+    partial[(size_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
 // partial: [G][T][2][C] (first S rows per group folded).  coef: [G][3][C].
 // Grid = (channel chunks of 16) x G.  dgamma/dbeta are summed over the groups
 // (one BatchNorm module, G calls): with G > 1 each block parks its group's sums
@@ -483,7 +568,12 @@ extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpo
   const int tpg = stf_bn_bwd_tiles(N, H, W, C, groups, dpool != nullptr);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(tpg * groups);
-  if (dpool)
+  static const bool lanes = [] { const char* e = getenv("STF_POOL_LANES"); return !(e && e[0] == '0'); }();
+  if (dpool && lanes && 64 % (C / 8) == 0 && mask_mode != 2 && (long)N * H * W < (1L << 31))
+    hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, grid, dim3(PNT), 0, s, (const uint16_t*)dz, dz_cstride,
+                       (const uint16_t*)dpool, (const uint16_t*)y, y_cstride, (long)N, H, W, C, groups, tpg, scale,
+                       shift, mean, invstd, mask_mode, (uint16_t*)g_out, partial);
+  else if (dpool)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride,
                        (const uint16_t*)dpool, (const uint16_t*)y, y_cstride, (long)N, H, W, C, groups, tpg, scale,
                        shift, mean, invstd, mask_mode, (const uint16_t*)mask_src, mask_cstride, (uint16_t*)g_out,

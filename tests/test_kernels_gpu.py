@@ -308,10 +308,10 @@ class _BN:
             self.bn.bias.uniform_(-0.5, 0.5)
 
 
-@pytest.mark.parametrize("pool", [False, True])
-def test_bn_forward_backward(pool):
+@pytest.mark.parametrize("pool,C", [(False, 64), (True, 64), (True, 128), (True, 512)])
+def test_bn_forward_backward(pool, C):
     from stfunet import nhwc
-    C, H = 64, 16
+    H = 16
     y = bfr(torch.randn(2, C, H, H, device=DEV) * 2 + 0.5)
     m = _BN(C)
     ref_bn = torch.nn.BatchNorm2d(C).to(DEV)
