@@ -32,7 +32,8 @@ class AdamW(torch.optim.Optimizer):
         params = group["params"]
         key = (gi, tuple(id(p) for p in params))
         fb = self._flat.get(gi)
-        if fb is not None and fb["key"] == key and fb["pptr"] == [p.data_ptr() for p in params]:
+        if fb is not None and fb["key"] == key and fb["pptr"][0] == params[0].data_ptr() and \
+                fb["pptr"][-1] == params[-1].data_ptr():
             return fb
         offs, off = [], 0
         for p in params:
@@ -45,22 +46,27 @@ class AdamW(torch.optim.Optimizer):
                          p.data_ptr() == base + 4 * o for p, o in zip(params, offs))
         m = torch.zeros(off, dtype=torch.float32, device=dev)
         v = torch.zeros(off, dtype=torch.float32, device=dev)
+        # one step counter shared by the group (every parameter steps together): the
+        # per-step bookkeeping is one fill_, not one per parameter (host-bound STF step)
+        step = torch.zeros((), dtype=torch.float32)
         for p, o in zip(params, offs):
             st = self.state[p]
             n = p.numel()
             if "exp_avg" in st:                       # resumed / pre-existing state
                 m[o:o + n].copy_(st["exp_avg"].reshape(-1))
                 v[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+            if "step" in st:
+                step.fill_(max(float(step), float(st["step"])))
             st["exp_avg"] = m[o:o + n].view(p.shape)
             st["exp_avg_sq"] = v[o:o + n].view(p.shape)
-            if "step" not in st:
-                st["step"] = torch.zeros((), dtype=torch.float32)
+            st["step"] = step
         pflat = None
         if contiguous:
             pflat = torch.empty(0, dtype=torch.float32, device=dev)
             pflat.set_(params[0].untyped_storage(), params[0].storage_offset(), (off,))
+        gptr = None
         fb = dict(key=key, pptr=[p.data_ptr() for p in params], offs=offs, n=off, m=m, v=v, p=pflat,
-                  gscratch=None)
+                  gscratch=None, step=step, gptr=gptr)
         self._flat[gi] = fb
         return fb
 
@@ -84,10 +90,8 @@ class AdamW(torch.optim.Optimizer):
                 raise RuntimeError("stfunet.optim.AdamW runs on the gfx950 kernel only (no CPU fallback)")
             fb = self._group_buffers(gi, group)
             b1, b2 = group["betas"]
-            st0 = self.state[params[0]]
-            step = int(st0["step"].item()) + 1
-            for p in params:
-                self.state[p]["step"].fill_(step)
+            step = int(fb["step"].item()) + 1
+            fb["step"].fill_(step)
             bc1 = 1.0 - b1 ** step
             bc2 = 1.0 - b2 ** step
             g = self._flat_grad(params, fb)
@@ -108,8 +112,14 @@ class AdamW(torch.optim.Optimizer):
         g0 = params[0].grad
         if g0 is not None:
             base = g0.data_ptr()
+            ptrs = [p.grad.data_ptr() if p.grad is not None else -1 for p in params]
+            if ptrs == fb["gptr"]:                    # the same flat gradient views as last step
+                g = torch.empty(0, dtype=torch.float32, device=g0.device)
+                g.set_(g0.untyped_storage(), g0.storage_offset(), (fb["n"],))
+                return g
             if all(p.grad is not None and p.grad.is_contiguous() and p.grad.data_ptr() == base + 4 * o
                    for p, o in zip(params, fb["offs"])):
+                fb["gptr"] = ptrs
                 g = torch.empty(0, dtype=torch.float32, device=g0.device)
                 g.set_(g0.untyped_storage(), g0.storage_offset(), (fb["n"],))
                 return g
