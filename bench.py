@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--time-steps", type=int, default=8)
     ap.add_argument("--pk", action="store_true", help="STF with 3 PK-map channels (configs[4])")
+    ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
+                    help="replay the training step as a HIP graph (N=1 only; auto = STF).  Off by default: "
+                         "measured slower than eager for STF (12.92 vs 12.49 ms/step), the replay loses most "
+                         "of the LSTM side-stream overlap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timer", action="store_true")
@@ -192,7 +196,11 @@ def main():
     else:
         model = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=args.time_steps, use_pk_maps=args.pk).to(dev)
     model.train()
-    opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.model == "stf" and world == 1)
+    if use_graph and world > 1:
+        raise SystemExit("--graph on needs N=1 (RCCL gradient buckets are not captured)")
+    opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8,
+                capturable=use_graph)
     steps_total = args.warmup + args.steps
     sched = engine.create_lr_scheduler(opt, max(steps_total, 1), 10, warmup=True)
     ddp = GradAllReduce(model) if world > 1 else None
@@ -235,9 +243,18 @@ def main():
     dominant = None
     if not args.no_kernel_timer:
         dominant = max(census, key=lambda k: census[k]["ms"]) if census else None
+    gstep = None
+    if use_graph:
+        from stfunet.graph import TrainStepGraph
+        loss = None                           # drop the last eager step's autograd graph before capture
+        gstep = TrainStepGraph(model, opt, engine.criterion, *batches[0]).capture()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if gstep is not None:                 # one replay = the whole step; lr published per step
+            loss = gstep.step(*batches[(args.warmup + i) % len(batches)])
+            sched.step()
+            continue
         if dominant is not None and i == args.steps - 1:
             nhwc.TIMER = nhwc.KernelTimer(only=dominant)
         loss = train_step(args.warmup + i)
@@ -245,6 +262,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if gstep is not None and dominant is not None:
+        # graph replays cannot be bracketed per launch: time the dominant kernel's launches
+        # in one eager step right after the timed region (same kernels, shapes, buffers)
+        nhwc.TIMER = nhwc.KernelTimer(only=dominant)
+        train_step(args.warmup + args.steps)
+        torch.cuda.synchronize()
     kt = nhwc.TIMER.summary() if nhwc.TIMER is not None else {}
     nhwc.TIMER = None
     last_loss = float(loss.item())
@@ -267,12 +290,15 @@ def main():
                     f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
                     f"{args.size}x{args.size} train step")
         roof = roofline(kt, workload, args.batch, census)
+        if gstep is not None and roof:
+            roof["timing"] = "dominant kernel timed in one eager step after the timed graph replays"
         res = {
             "metric": "training samples/sec (256x256 DCE-MRI frames)",
             "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
+            "execution": "hip_graph" if gstep is not None else "eager",
             "config": {"workload": workload,
                        "model": "UNet" if args.model == "unet" else "STFLSTMUNet",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,

@@ -263,6 +263,11 @@ int stf_loss_bwd(const float* logits, const int64_t* target, int N, int H, int W
 int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
               float beta1, float beta2, float eps, float weight_decay, float bc1,
               float bc2, stf_stream_t stream);
+/* Graph-capturable AdamW: hyper = DEVICE {lr, step} (step = this update's count,
+ * already incremented); bias corrections computed on the device exactly as the host
+ * computes them for stf_adamw. */
+int stf_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                  float beta1, float beta2, float eps, float weight_decay, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- layout
  * x [N][C][H][W] fp32 -> NHWC bf16 with Cpad (>= C, multiple of 8) channels,

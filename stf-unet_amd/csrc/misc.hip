@@ -145,6 +145,40 @@ long grid_for(long units, long cap) {
 
 }  // namespace
 
+// Graph-capturable variant: lr and the step count come from device memory (hyper[0] =
+// lr, hyper[1] = step after this update's increment), so a captured training step can
+// be replayed with the schedule's new lr (written between replays) and a step count
+// that advances on the device.  Bias corrections in double, rounded to fp32 exactly as
+// the host computes them for stf_adamw, so both paths produce the same bits.
+__global__ void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, long n, const float* __restrict__ hyper, float b1, float b2,
+                                 float eps, float wd) {
+  const float lr = hyper[0];
+  const double step = hyper[1];
+  const float bc1 = (float)(1.0 - pow((double)b1, step)), bc2 = (float)(1.0 - pow((double)b2, step));
+  const float step_size = lr / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    float pp = p[i] * (1.f - lr * wd);
+    const float gg = g[i];
+    const float mm = m[i] + (1.f - b1) * (gg - m[i]);
+    const float ww = b2 * v[i] + (1.f - b2) * gg * gg;
+    pp -= step_size * mm / (sqrtf(ww) * inv_sqrt_bc2 + eps);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = ww;
+  }
+}
+
+extern "C" int stf_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, float beta1,
+                             float beta2, float eps, float weight_decay, stf_stream_t stream) {
+  if (n < 0 || !hyper) return STF_EINVAL;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 4096)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (long)n,
+                     hyper, beta1, beta2, eps, weight_decay);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
                          float eps, float weight_decay, float bc1, float bc2, stf_stream_t stream) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return STF_EINVAL;

@@ -23,10 +23,30 @@ def _align4(n):
 
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, fused=None,
-                 **unused):
+                 capturable=False, **unused):
+        """``capturable=True``: lr and the step count live on the device ({lr, step}
+        per group, ``stf_adamw_dev``), so ``step()`` can be captured in a HIP graph
+        (``stfunet.graph``); call ``graph_sync()`` after the LR scheduler and before
+        each replay to publish the new lr.  Same arithmetic as the host-scalar path."""
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._flat = {}
+        self.capturable = capturable
+        self._hyper = {}
+
+    def _hyper_of(self, gi, group, fb):
+        h = self._hyper.get(gi)
+        if h is None:
+            h = self._hyper[gi] = torch.zeros(2, dtype=torch.float32, device=fb["m"].device)
+            h[1] = float(fb["step"])
+        return h
+
+    def graph_sync(self):
+        """Publish every group's current lr to the device (outside graph capture)."""
+        for gi, group in enumerate(self.param_groups):
+            h = self._hyper.get(gi)
+            if h is not None:
+                h[0:1].fill_(float(group["lr"]))
 
     def _group_buffers(self, gi, group):
         params = group["params"]
@@ -90,6 +110,18 @@ class AdamW(torch.optim.Optimizer):
                 raise RuntimeError("stfunet.optim.AdamW runs on the gfx950 kernel only (no CPU fallback)")
             fb = self._group_buffers(gi, group)
             b1, b2 = group["betas"]
+            if self.capturable:
+                h = self._hyper_of(gi, group, fb)
+                if not torch.cuda.is_current_stream_capturing():
+                    h[0:1].fill_(float(group["lr"]))
+                    fb["step"].fill_(int(fb["step"].item()) + 1)    # host mirror (state_dict)
+                h[1:2].add_(1.0)
+                g = self._flat_grad(params, fb)
+                pf = fb["p"]
+                assert pf is not None, "capturable AdamW needs the model's flat parameters"
+                call("stf_adamw_dev", _p(pf), _p(g), _p(fb["m"]), _p(fb["v"]), fb["n"], _p(h), float(b1), float(b2),
+                     float(group["eps"]), float(group["weight_decay"]), stream())
+                continue
             step = int(fb["step"].item()) + 1
             fb["step"].fill_(step)
             bc1 = 1.0 - b1 ** step
