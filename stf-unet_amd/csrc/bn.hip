@@ -47,11 +47,11 @@ int tiles_per_group(long units_per_group, int groups) {
 // group.  With G > 1 the running statistics must see the G updates in order:
 // each block parks (mean, biased var) in row 0 of its group (scratch) and
 // bn_running_kernel applies them sequentially.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(float* __restrict__ stats, int S, int T, int G, int C,
+__global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __restrict__ stats, int S, int T, int G, int C,
                                                         long Mg, const float* gamma, const float* beta, float mom,
                                                         float eps, float* rm, float* rv, float* mean, float* invstd,
                                                         float* scale, float* shift) {
-  __shared__ double red[256];
+  __shared__ double red[stf::FOLD_NT];
   const int g = blockIdx.y;
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
@@ -360,11 +360,11 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
 // Grid = (channel chunks of 16) x G.  dgamma/dbeta are summed over the groups
 // (one BatchNorm module, G calls): with G > 1 each block parks its group's sums
 // in row 0 of the group and bn_bwd_groupsum_kernel adds them in order.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
+__global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
                                                             int C, long Mg, const float* gamma, const float* mean,
                                                             const float* invstd, float* dgamma, float* dbeta,
                                                             float* coef) {
-  __shared__ double red[256];
+  __shared__ double red[stf::FOLD_NT];
   const int g = blockIdx.y;
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
@@ -493,9 +493,9 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* 
 
 // sum over tiles of partial[t][C] -> out[C] (fixed order); shared with misc.hip / loss.hip
 // launch: grid ceil(C/16), 256 threads (16 channels x 16 row-lanes)
-__global__ __launch_bounds__(256) void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C,
+__global__ __launch_bounds__(stf::FOLD_NT) void stf_tile_sum_kernel(const float* __restrict__ partial, int tiles, int C,
                                                          float* __restrict__ out) {
-  __shared__ double red[256];
+  __shared__ double red[stf::FOLD_NT];
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C;
   const double s = stf::fold16_finish(stf::fold16_partial(partial, tiles, C, c, cok), red);
@@ -511,7 +511,7 @@ extern "C" int stf_bn_finalize(float* stats, int tiles, int groups, int C, int64
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
   const int S = stats ? stf::colsum_stage1(stats, tiles, 2L * C, s, groups, stf::FOLD16_ROWS) : 0;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, stats, S, tiles, groups, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16, groups), dim3(stf::FOLD_NT), 0, s, stats, S, tiles, groups, C,
                      (long)(M / groups), gamma, beta, momentum, eps, running_mean, running_var, mean, invstd,
                      scale, shift);
   STF_CHECK_LAUNCH();
@@ -593,7 +593,7 @@ extern "C" int stf_bn_bwd_finalize(float* partial, int tiles, int groups, int C,
   hipStream_t s = (hipStream_t)stream;
   if (groups < 1 || M % groups) return STF_EINVAL;
   const int S = stf::colsum_stage1(partial, tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16, groups), dim3(256), 0, s, partial, S, tiles, groups,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16, groups), dim3(stf::FOLD_NT), 0, s, partial, S, tiles, groups,
                      C, (long)(M / groups), gamma, mean, invstd, dgamma, dbeta, coef);
   STF_CHECK_LAUNCH();
   if (groups > 1 && (dgamma || dbeta)) {
@@ -652,7 +652,7 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
     const int S = stf::colsum_stage1(bias_partial, tiles, C, s, 1, stf::FOLD16_ROWS);
-    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(256), 0, s, bias_partial, S, C, dbias);
+    hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
   return 0;

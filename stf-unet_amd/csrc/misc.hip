@@ -227,7 +227,7 @@ extern "C" int stf_channel_sum(const void* x, int x_cstride, int M, int C, float
                      partial);
   STF_CHECK_LAUNCH();
   const int S = stf::colsum_stage1(partial, tiles, C, s, 1, stf::FOLD16_ROWS);
-  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(256), 0, s, partial, S, C, out);
+  hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, s, partial, S, C, out);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -41,22 +41,24 @@ static inline int colsum_stage1(float* buf, long T, long W, hipStream_t st, int 
   return S;
 }
 
-// Row folding inside one 256-thread block: 16 row-lanes x 16 columns.  Column
-// c = blockIdx.x * 16 + (tid & 15); lane r = tid >> 4 sums rows r, r+16, ... < S
-// of base[t * stride + c] (fp64); fold16_finish returns the total (fixed order)
-// on lane 0.  Consumers (finalize kernels) read <= a few hundred rows this way
-// without a separate folding launch.
+// Row folding inside one block: 16 columns x (blockDim / 16) row-lanes.  Column
+// c = blockIdx.x * 16 + (tid & 15); lane r = tid >> 4 sums rows r, r+RL, ... < S
+// (RL = blockDim / 16 row-lanes) of base[t * stride + c] (fp64); fold16_finish returns
+// the total (fixed order) on lane 0 (threads 0..15).  The finalize kernels run 1024
+// threads (64 row-lanes): their fold is a latency chain, ~4 dependent loads per lane
+// instead of ~16 at 256 threads.  ``red`` holds blockDim doubles.
 STF_DEV double fold16_partial(const float* base, int S, long stride, long c, bool cok) {
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;       // four chains: the loads pipeline
   if (cok) {
+    const int RL = blockDim.x >> 4;
     int t = threadIdx.x >> 4;
-    for (; t + 48 < S; t += 64) {
+    for (; t + 3 * RL < S; t += 4 * RL) {
       a0 += base[(long)t * stride + c];
-      a1 += base[(long)(t + 16) * stride + c];
-      a2 += base[(long)(t + 32) * stride + c];
-      a3 += base[(long)(t + 48) * stride + c];
+      a1 += base[(long)(t + RL) * stride + c];
+      a2 += base[(long)(t + 2 * RL) * stride + c];
+      a3 += base[(long)(t + 3 * RL) * stride + c];
     }
-    for (; t < S; t += 16) a0 += base[(long)t * stride + c];
+    for (; t < S; t += RL) a0 += base[(long)t * stride + c];
   }
   return (a0 + a1) + (a2 + a3);
 }
@@ -65,11 +67,14 @@ STF_DEV double fold16_finish(double v, double* red) {
   red[threadIdx.x] = v;
   __syncthreads();
   double tot = 0.0;
+  const int RL = blockDim.x >> 4;
   if ((threadIdx.x >> 4) == 0)
-    for (int r = 0; r < 16; ++r) tot += red[r * 16 + (threadIdx.x & 15)];
+    for (int r = 0; r < RL; ++r) tot += red[r * 16 + (threadIdx.x & 15)];
   __syncthreads();
   return tot;
 }
+
+constexpr int FOLD_NT = 1024;         // block size of the fold16 consumers (finalize kernels)
 
 constexpr long FOLD16_ROWS = 1024;    // finalize kernels read up to this many rows directly
 
