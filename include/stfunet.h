@@ -294,6 +294,13 @@ typedef struct stf_pack_desc {
   int d0, d1, R, S, mode, cpad;
 } stf_pack_desc;
 int stf_pack_weights(const stf_pack_desc* descs, int count, int64_t max_elems, stf_stream_t stream);
+/* Same job through LDS-tiled transposes (whole source rows read, 16-B output
+ * chunks written).  stf_pack_tiles(d0,d1,R,S,mode,cpad) = the tile count of one
+ * descriptor, or -1 when the tiled kernel cannot take it (R*S > 9, or output rows
+ * not a multiple of 8 elements); max_tiles = the largest count in the list (every
+ * descriptor must have one >= 0).  ABI v5. */
+int stf_pack_tiles(int d0, int d1, int R, int S, int mode, int cpad);
+int stf_pack_weights_tiled(const stf_pack_desc* descs, int count, int max_tiles, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- STF-LSTM-UNet
  * x [B][Ttot][C][H][W] fp32 -> t-major NHWC bf16 [T*B][H][W][Cpad]: frame t of

@@ -113,6 +113,85 @@ __global__ void pack_weights_kernel(const stf_pack_desc* __restrict__ descs) {
     reinterpret_cast<bf16*>(d.out)[o] = f2bf(pack_src(d.w, d.d0, d.d1, d.R, d.S, d.mode, d.cpad, o));
 }
 
+// Tiled packing (every descriptor of the list in one launch; blockIdx.y = descriptor).
+// Source w is [A = d0][Bc = d1][RS] fp32.  Modes whose rows run along A (1, 5: Conv
+// dgrad rows [ci][tap][co]; 2, 4: ConvT rows over ci) transpose 64 (a) x 16 (b) x RS
+// tiles through LDS; modes whose rows run along b (0: [co][tap][ci(pad)], 3: [ci][tap]
+// [co]) transpose per-a [b][tap] blocks (4 a x 64 b).  Reads are whole source rows,
+// writes are 16-B chunks of output rows (the element-wise gather above reads one
+// scattered float per output: ~1.3 TB/s effective, 0.28 ms per cfg2 step).
+constexpr int PK_TA = 64, PK_TB = 16, PK_IA = 4, PK_IB = 64, PK_MAXRS = 9;
+
+STF_DEV bool pack_outer(int mode) { return mode == 1 || mode == 5 || mode == 2 || mode == 4; }
+
+// output row (the index before the innermost a-run) of source element (b, tap) in the
+// A-major modes
+STF_DEV long pack_outer_row(int mode, int b, int tap, int d1, int RS) {
+  if (mode == 1 || mode == 4) return (long)b * RS + tap;
+  if (mode == 5) return (long)b * RS + (RS - 1 - tap);
+  return (long)tap * d1 + b;                                   // mode 2: [(tap)*Co + co][Ci]
+}
+
+STF_DEV int pack_tiles(const stf_pack_desc& d) {
+  const int bext = d.mode == 0 ? d.cpad : d.d1;
+  return pack_outer(d.mode) ? ((d.d0 + PK_TA - 1) / PK_TA) * ((d.d1 + PK_TB - 1) / PK_TB)
+                            : ((d.d0 + PK_IA - 1) / PK_IA) * ((bext + PK_IB - 1) / PK_IB);
+}
+
+__global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __restrict__ descs) {
+  __shared__ float tile[PK_TA * (PK_TB * PK_MAXRS + 1)];
+  const stf_pack_desc d = descs[blockIdx.y];
+  if ((int)blockIdx.x >= pack_tiles(d)) return;
+  const int RS = d.R * d.S, tid = threadIdx.x;
+  uint16_t* out = reinterpret_cast<uint16_t*>(d.out);
+  if (pack_outer(d.mode)) {
+    const int nbb = (d.d1 + PK_TB - 1) / PK_TB;
+    const int a0 = (blockIdx.x / nbb) * PK_TA, b0 = (blockIdx.x % nbb) * PK_TB;
+    const int na = min(PK_TA, d.d0 - a0), nb = min(PK_TB, d.d1 - b0), cols = nb * RS, LS = PK_TB * PK_MAXRS + 1;
+    for (int e = tid; e < na * cols; e += NT) {                // whole source rows: [a][b0..b0+nb)[tap]
+      const int a = e / cols, c = e - a * cols;
+      tile[a * LS + c] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+    }
+    __syncthreads();
+    const int qn = (na + 7) / 8;                               // 8-element chunks along a
+    for (int e = tid; e < cols * qn; e += NT) {
+      const int c = e / qn, q = e - c * qn, b = c / RS, tap = c - b * RS;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (q * 8 + j < na) ? tile[(q * 8 + j) * LS + c] : 0.f;
+      uint16_t* o = out + pack_outer_row(d.mode, b0 + b, tap, d.d1, RS) * d.d0 + a0 + q * 8;
+      if (q * 8 + 8 <= na) *reinterpret_cast<uint4*>(o) = pack8(v);
+      else
+        for (int j = 0; j < na - q * 8; ++j) reinterpret_cast<bf16*>(o)[j] = f2bf(v[j]);
+    }
+  } else {
+    const int bext = d.mode == 0 ? d.cpad : d.d1;              // mode 0 rows are cpad wide (zero pad)
+    const int nbb = (bext + PK_IB - 1) / PK_IB;
+    const int a0 = (blockIdx.x / nbb) * PK_IA, b0 = (blockIdx.x % nbb) * PK_IB;
+    const int na = min(PK_IA, d.d0 - a0), nb = min(PK_IB, bext - b0), LS = PK_IB * PK_MAXRS + 1;
+    const int nbs = max(0, min(nb, d.d1 - b0));                // source columns present
+    for (int e = tid; e < na * nbs * RS; e += NT) {
+      const int a = e / (nbs * RS), c = e - a * nbs * RS;
+      tile[a * LS + c] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+    }
+    __syncthreads();
+    const int qn = (nb + 7) / 8;
+    for (int e = tid; e < na * RS * qn; e += NT) {
+      const int a = e / (RS * qn), r = e - a * RS * qn, tap = r / qn, q = r - tap * qn;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int b = q * 8 + j;
+        v[j] = (b < nbs) ? tile[a * LS + b * RS + tap] : 0.f;
+      }
+      uint16_t* o = out + ((long)(a0 + a) * RS + tap) * bext + b0 + q * 8;
+      if (q * 8 + 8 <= nb) *reinterpret_cast<uint4*>(o) = pack8(v);
+      else
+        for (int j = 0; j < nb - q * 8; ++j) reinterpret_cast<bf16*>(o)[j] = f2bf(v[j]);
+    }
+  }
+}
+
 __global__ void channel_sum_kernel(const uint16_t* __restrict__ x, int xcs, long M, int C,
                                    float* __restrict__ partial) {
   __shared__ float red[NT][9];
@@ -209,6 +288,26 @@ extern "C" int stf_pack_weight(const float* w, int d0, int d1, int R, int S, int
   return 0;
 }
 
+extern "C" int stf_pack_tiles(int d0, int d1, int R, int S, int mode, int cpad) {
+  // tiles of the tiled packing kernel for one descriptor, or -1 when it needs the
+  // element-wise kernel (output rows not 8-aligned, RS > 9)
+  const int RS = R * S;
+  if (RS > PK_MAXRS || mode < 0 || mode > 5) return -1;
+  const bool outer = mode == 1 || mode == 5 || mode == 2 || mode == 4;
+  const int bext = mode == 0 ? cpad : d1;
+  if (outer ? (d0 % 8) : (bext % 8)) return -1;
+  return outer ? ((d0 + PK_TA - 1) / PK_TA) * ((d1 + PK_TB - 1) / PK_TB)
+               : ((d0 + PK_IA - 1) / PK_IA) * ((bext + PK_IB - 1) / PK_IB);
+}
+
+extern "C" int stf_pack_weights_tiled(const stf_pack_desc* descs, int count, int max_tiles, stf_stream_t stream) {
+  if (count <= 0) return 0;
+  if (max_tiles <= 0 || count > 65535) return STF_EINVAL;
+  hipLaunchKernelGGL(pack_tiled_kernel, dim3((unsigned)max_tiles, count), dim3(NT), 0, (hipStream_t)stream, descs);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int stf_pack_weights(const stf_pack_desc* descs, int count, int64_t max_elems, stf_stream_t stream) {
   if (count <= 0) return 0;
   if (count > 65535 || max_elems <= 0 || max_elems >= (1L << 31)) return STF_EINVAL;
@@ -237,4 +336,4 @@ extern "C" const char* stf_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-extern "C" int stf_abi_version(void) { return 4; }
+extern "C" int stf_abi_version(void) { return 5; }

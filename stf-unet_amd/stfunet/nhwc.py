@@ -9,6 +9,7 @@ walks off a buffer can take the whole GPU down) and launches on torch's
 current stream.  Workspaces come from torch's caching allocator.
 """
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -195,17 +196,24 @@ class PackCache:
             return
         if self._desc is None or self._desc[0] != self.recorded:
             arr = (_PackDesc * len(self.recorded))()
-            mx = 0
+            mx, tiles = 0, 0
             for i, key in enumerate(self.recorded):
                 w, buf, mode, cpad = self.bufs[key]
                 d0, d1, R, S = w.shape
                 arr[i] = _PackDesc(w.data_ptr(), buf.data_ptr(), d0, d1, R, S, mode, cpad)
                 mx = max(mx, buf.numel())
+                nt = _lib.load().stf_pack_tiles(d0, d1, R, S, mode, cpad)
+                tiles = max(tiles, nt) if tiles >= 0 and nt >= 0 else -1
+            if os.environ.get("STF_PACK_TILED", "1") == "0":
+                tiles = -1
             dev = self.bufs[self.recorded[0]][1].device
             t = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
-            self._desc = (self.recorded, t, mx)
-        _, t, mx = self._desc
-        call("stf_pack_weights", _p(t), len(self.recorded), mx, stream())
+            self._desc = (self.recorded, t, mx, tiles)
+        _, t, mx, tiles = self._desc
+        if tiles > 0:           # LDS-tiled transposes (every descriptor qualifies)
+            call("stf_pack_weights_tiled", _p(t), len(self.recorded), tiles, stream())
+        else:
+            call("stf_pack_weights", _p(t), len(self.recorded), mx, stream())
         self.fresh = set(self.recorded)
 
     def get(self, w, mode, cpad):

@@ -434,11 +434,22 @@ def test_adamw_flat_matches_oracle():
     assert rel(p0, pr) < 1e-6 and rel(m, mr) < 1e-6 and rel(v, vr) < 1e-6
 
 
-def test_pack_weights_batched_matches_single():
-    """stf_pack_weights (one launch, every layout) == stf_pack_weight per tensor, bit for bit."""
+PACK_JOBS = [((64, 8, 3, 3), 0, 8), ((128, 64, 3, 3), 0, 64), ((64, 128, 3, 3), 5, 0), ((64, 32, 3, 3), 1, 0),
+             ((256, 128, 2, 2), 2, 0), ((256, 128, 2, 2), 3, 0), ((64, 32, 3, 3), 4, 0), ((96, 40, 1, 1), 0, 48)]
+# ragged tiles (d0 not a multiple of 64 / 4, d1 not of 16 / 64), the stem's 49-column
+# 1x1 view padded to 64, wide 1x1 / 3x3 layers
+PACK_RAGGED = [((72, 20, 3, 3), 5, 0), ((72, 20, 3, 3), 1, 0), ((40, 72, 2, 2), 2, 0), ((40, 72, 2, 2), 3, 0),
+               ((72, 24, 3, 3), 4, 0), ((64, 49, 1, 1), 0, 64), ((66, 130, 3, 3), 0, 136), ((512, 1024, 3, 3), 5, 0),
+               ((1024, 512, 1, 1), 1, 0)]
+
+
+@pytest.mark.parametrize("tiled,jobs", [("1", PACK_JOBS), ("0", PACK_JOBS), ("1", PACK_RAGGED),
+                                        ("1", PACK_RAGGED + [((32, 16, 5, 5), 0, 16)])])
+def test_pack_weights_batched_matches_single(monkeypatch, tiled, jobs):
+    """stf_pack_weights(_tiled) (one launch, every layout) == stf_pack_weight per tensor, bit
+    for bit (the last list has a 5x5 kernel: the whole list takes the element-wise kernel)."""
     from stfunet import nhwc
-    jobs = [((64, 8, 3, 3), 0, 8), ((128, 64, 3, 3), 0, 64), ((64, 128, 3, 3), 5, 0), ((64, 32, 3, 3), 1, 0),
-            ((256, 128, 2, 2), 2, 0), ((256, 128, 2, 2), 3, 0), ((64, 32, 3, 3), 4, 0), ((96, 40, 1, 1), 0, 48)]
+    monkeypatch.setenv("STF_PACK_TILED", tiled)
     cache = nhwc.PackCache()
     ws = [torch.randn(*shape, device=DEV) for shape, _, _ in jobs]
     nhwc.ACTIVE_PACKS = cache
