@@ -377,6 +377,46 @@ int stf_tofts_fit(const float* curves, int P, int T, const float* time_points, c
                   int batch, int epochs, const float* adam_sched, float beta1, float beta2, float eps,
                   const float* bounds, float* params, stf_stream_t stream);
 
+/* ---------------------------------------------------------------- training augmentation
+ * Replaces the per-sample CPU transforms of the reference's DataLoader workers
+ * (transforms.py:18-157 as composed by train.py:51-73 get_transform; my_dataset.py:
+ * 200-239 applies them per frame): RandomResize (Pillow bilinear / nearest) ->
+ * RandomHorizontalFlip -> RandomVerticalFlip -> RandomRotation (Pillow bilinear /
+ * nearest, expand=False) -> RandomCrop (zero pad) -> ToTensor + Normalize, bit-exact
+ * to Pillow 12's integer / double arithmetic.  The host draws the random parameters
+ * (Python `random`, the reference's draw order), builds Pillow's coefficient tables
+ * and fills one descriptor per frame / mask; sources of any sizes sit in one uint8
+ * arena (src offsets in bytes).
+ *
+ * frames: coefficient rows at coef[cx + j*(kx+2)] = {xmin, n, k_0..k_{kx-1}} for
+ * output column j (likewise cy/ky for rows; 22-bit fixed point, Pillow
+ * ImagingResample); the resized H2 x W2 image goes to scratch[rs]; the output
+ * window oh x ow (crop origin h0, w0 in the zero-padded rotated image) is written
+ * as fp32 (v/255 - mean)/std at out[out + y*ow + x].  m = Image.rotate's inverse
+ * affine (double), used when flags & STF_AUG_ROTATE.
+ * masks: cx / cy index int tables of W2 / H2 source columns / rows (-1 = outside,
+ * Pillow ImagingScaleAffine), fx = {a0, a1, a3, a4, xo, yo} 16.16 fixed-point
+ * rotation; output int64.
+ * max_resized_px / max_out_px = largest H2*W2 / oh*ow in the list (grid size). */
+#define STF_AUG_HFLIP 1
+#define STF_AUG_VFLIP 2
+#define STF_AUG_ROTATE 4
+typedef struct stf_aug_frame {
+  int64_t src, rs, out;
+  int H, W, H2, W2;
+  int cx, cy, kx, ky;
+  int oh, ow, h0, w0;
+  int flags;
+  int fx[6];
+  int pad_;
+  double m[6];
+} stf_aug_frame;
+int stf_augment_frames(const uint8_t* src, const stf_aug_frame* frames, int n, const int* coef,
+                       uint8_t* scratch, int max_resized_px, int max_out_px, float mean, float stdv,
+                       float* out, stf_stream_t stream);
+int stf_augment_masks(const uint8_t* src, const stf_aug_frame* masks, int n, const int* tabs,
+                      int max_out_px, int64_t* out, stf_stream_t stream);
+
 const char* stf_error_string(int code);
 int stf_abi_version(void);
 

@@ -81,6 +81,8 @@ _SIGS = {
     "stf_pack_input": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weights": (c_int, [P, c_int, c_int64, P]),
+    "stf_augment_frames": (c_int, [P, P, c_int, P, P, c_int, c_int, c_float, c_float, P, P]),
+    "stf_augment_masks": (c_int, [P, P, c_int, P, c_int, P, P]),
     "stf_pack_tiles": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "stf_pack_weights_tiled": (c_int, [P, c_int, c_int, P]),
     "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
