@@ -123,7 +123,9 @@ class DeviceAugment:
         self.mean, self.std = float(mean), float(std)
         self.hflip_prob, self.vflip_prob, self.degrees = hflip_prob, vflip_prob, degrees
         self.paired = paired
-        self.rng = random.Random(seed)
+        # seed None: the global ``random`` module, as the reference draws (DataLoader
+        # workers reseed it per worker); else a private generator
+        self.rng = random.Random(seed) if seed is not None else random
         self.device = torch.device(device) if device is not None else torch.device("cuda")
 
     # ------------------------------------------------------------- draws (train.py:58-63 order)
@@ -149,6 +151,14 @@ class DeviceAugment:
 
     # ------------------------------------------------------------- launch
     def __call__(self, frames, masks, params=None, launch=True):
+        """plan + to_device (+ launch)."""
+        st = self.to_device(self.plan(frames, masks, params))
+        return self.launch(st) if launch else st
+
+    def plan(self, frames, masks, params=None):
+        """Host half (numpy only, picklable: runs in DataLoader workers via
+        ``DriveDataset.collate_fn``): draws, Pillow tables, descriptors, and ONE byte
+        blob = [sources | int tables | descriptors] for a single H2D copy."""
         B = len(frames)
         if B == 0:
             raise ValueError("empty batch")
@@ -226,34 +236,44 @@ class DeviceAugment:
             srcs.append(masks[b].reshape(-1))
             off += H * W
 
-        dev = self.device
-        host = torch.from_numpy(np.concatenate(srcs)).pin_memory()
-        src = host.to(dev, non_blocking=True)
-        ints = torch.from_numpy(np.concatenate(coef_parts + near_parts).astype(np.int32)).pin_memory()
-        ints = ints.to(dev, non_blocking=True)
-        near_base = coef_len
         for b in range(B):                                  # mask tables follow the coefficients
-            mdesc[b].cx += near_base
-            mdesc[b].cy += near_base
-        desc = torch.frombuffer(bytearray(bytes(fdesc) + bytes(mdesc)), dtype=torch.uint8).pin_memory()
-        desc = desc.to(dev, non_blocking=True)
-        scratch = torch.empty(max(rs_off, 1), dtype=torch.uint8, device=dev)
-        oh, ow = out_hw
-        x = torch.empty(B, F, 1, oh, ow, dtype=torch.float32, device=dev)
-        target = torch.empty(B, oh, ow, dtype=torch.int64, device=dev)
-        staged = dict(src=src, desc=desc, ints=ints, scratch=scratch, x=x, target=target, n=B * F, B=B,
-                      mask_desc=ctypes.sizeof(fdesc), max_rs=max_rs, max_out=max_out)
-        # staging buffers: device ones are stream-ordered on this stream; the pinned host
-        # ones are held by torch's host allocator until their copies have completed
-        return self.launch(staged) if launch else staged
+            mdesc[b].cx += coef_len
+            mdesc[b].cy += coef_len
+
+        def al(n):
+            return (n + 15) // 16 * 16
+        ints = np.concatenate(coef_parts + near_parts).astype(np.int32).view(np.uint8)
+        dbytes = np.frombuffer(bytes(fdesc) + bytes(mdesc), np.uint8)
+        o_int = al(off)
+        o_desc = al(o_int + ints.size)
+        blob = np.zeros(o_desc + dbytes.size, np.uint8)
+        blob[:off] = np.concatenate(srcs)
+        blob[o_int:o_int + ints.size] = ints
+        blob[o_desc:] = dbytes
+        return dict(blob=blob, o_int=o_int, o_desc=o_desc, mask_desc=ctypes.sizeof(fdesc), n=B * F, B=B, F=F,
+                    out_hw=out_hw, rs_bytes=rs_off, max_rs=max_rs, max_out=max_out)
+
+    def to_device(self, plan):
+        """One pinned H2D copy of the plan's blob + the output buffers (main process)."""
+        dev = self.device
+        blob = torch.from_numpy(plan["blob"]).pin_memory().to(dev, non_blocking=True)
+        base = blob.data_ptr()
+        B, F, (oh, ow) = plan["B"], plan["F"], plan["out_hw"]
+        # the pinned host copy is held by torch's host allocator until the copy completes;
+        # device buffers are ordered on this stream
+        return dict(blob=blob, src=base, ints=base + plan["o_int"], desc=base + plan["o_desc"],
+                    mask_desc=plan["mask_desc"], n=plan["n"], B=B, max_rs=plan["max_rs"], max_out=plan["max_out"],
+                    scratch=torch.empty(max(plan["rs_bytes"], 1), dtype=torch.uint8, device=dev),
+                    x=torch.empty(B, F, 1, oh, ow, dtype=torch.float32, device=dev),
+                    target=torch.empty(B, oh, ow, dtype=torch.int64, device=dev))
 
     def launch(self, st):
-        """The three kernels over a staged batch (``__call__(..., launch=False)``)."""
+        """The three kernels over a batch on the device (``__call__(..., launch=False)``)."""
         s = stream()
-        call("stf_augment_frames", st["src"].data_ptr(), st["desc"].data_ptr(), st["n"], st["ints"].data_ptr(),
-             st["scratch"].data_ptr(), st["max_rs"], st["max_out"], self.mean, self.std, st["x"].data_ptr(), s)
-        call("stf_augment_masks", st["src"].data_ptr(), st["desc"].data_ptr() + st["mask_desc"], st["B"],
-             st["ints"].data_ptr(), st["max_out"], st["target"].data_ptr(), s)
+        call("stf_augment_frames", st["src"], st["desc"], st["n"], st["ints"], st["scratch"].data_ptr(),
+             st["max_rs"], st["max_out"], self.mean, self.std, st["x"].data_ptr(), s)
+        call("stf_augment_masks", st["src"], st["desc"] + st["mask_desc"], st["B"], st["ints"], st["max_out"],
+             st["target"].data_ptr(), s)
         return st["x"], st["target"]
 
     @staticmethod

@@ -97,3 +97,26 @@ def test_rejects_mixed_output_sizes():
     masks = [np.zeros((240, 300), np.uint8), np.zeros((256, 256), np.uint8)]
     with pytest.raises(ValueError):
         ev(frames, masks)
+
+
+def test_device_loader_matches_oracle(tmp_path):
+    """DriveDataset -> DataLoader (plans built in the batch) -> DeviceLoader, against the
+    oracle applied to the same decoded frames with the same draws."""
+    import torch.utils.data
+    from _dataset_util import make_tree
+    from stfunet.augment import DeviceAugment
+    from stfunet.dataset import DeviceLoader, DriveDataset
+    make_tree(str(tmp_path), size=(200, 260))
+    ds = DriveDataset(str(tmp_path), "train", transforms=DeviceAugment(seed=9, device="cuda"), use_pk_maps=True)
+    loader = DeviceLoader(torch.utils.data.DataLoader(ds, batch_size=2, collate_fn=ds.collate_fn), ds.transforms)
+    twin = DeviceAugment(seed=9, device="cpu")
+    i = 0
+    for x, t in loader:
+        x, t = x.cpu(), t.cpu()
+        for b in range(x.shape[0]):
+            frames, mask = ds._raw(i)
+            params = twin.draw_sample(*frames.shape)
+            want_x, want_t = A.sample(frames, mask, params)
+            assert torch.equal(x[b], torch.from_numpy(want_x)) and torch.equal(t[b], torch.from_numpy(want_t))
+            i += 1
+    assert i == len(ds)
