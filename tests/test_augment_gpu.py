@@ -120,3 +120,25 @@ def test_device_loader_matches_oracle(tmp_path):
             assert torch.equal(x[b], torch.from_numpy(want_x)) and torch.equal(t[b], torch.from_numpy(want_t))
             i += 1
     assert i == len(ds)
+
+
+def test_train_one_epoch_from_device_loader(tmp_path):
+    """The device-augmented loader is a drop-in for the reference's DataLoader: one epoch
+    of engine.train_one_epoch (UNet in=8, flat channels) over it, finite loss."""
+    import torch.utils.data
+    from _dataset_util import make_tree
+    from stfunet import engine
+    from stfunet.augment import DeviceAugment
+    from stfunet.dataset import DeviceLoader, DriveDataset
+    from stfunet.optim import AdamW
+    from stfunet.unet import UNet
+    make_tree(str(tmp_path), n_patients=2, slices=2, size=(160, 160), pk=False)
+    ds = DriveDataset(str(tmp_path), "train", transforms=DeviceAugment(seed=2, device="cuda"))
+    loader = DeviceLoader(torch.utils.data.DataLoader(ds, batch_size=2, shuffle=True, collate_fn=ds.collate_fn),
+                          ds.transforms)
+    model = UNet(in_channels=8, num_classes=2, base_c=16).cuda()
+    opt = AdamW([q for q in model.parameters() if q.requires_grad], lr=1e-3, weight_decay=1e-4)
+    sched = engine.create_lr_scheduler(opt, len(loader), 1, warmup=True)
+    loss, lr = engine.train_one_epoch(model, opt, loader, torch.device("cuda"), 0, 2, lr_scheduler=sched,
+                                      print_freq=100)
+    assert np.isfinite(loss) and lr > 0
