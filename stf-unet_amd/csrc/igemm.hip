@@ -44,6 +44,11 @@ STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
 
 STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
+#ifndef STF_LSTM_STAGED
+#define STF_LSTM_STAGED 1
+#endif
+STF_DEV constexpr bool lstm_staged() { return STF_LSTM_STAGED != 0; }
+
 // Shared epilogue: acc[i][j][r] = pixel mrow[i] (this lane's GEMM row of
 // fragment i, -1 = outside the image / tile), channel n0 + wn*WTN + j*16 +
 // (lane>>4)*4 + r.  `tile` indexes the BatchNorm partial-statistics row.
@@ -245,6 +250,71 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
       if (((cc - first + CPR) % CPR) < CW) t += red[(w * 2 + q) * BN + cl];
     }
     a.stats[(size_t)tile * 2 * a.Nout + q * a.Nout + n0 + cl] = t;
+  }
+}
+
+// LSTM cell epilogue of the DMA kernels, staged through LDS: the block's c_prev tile
+// [BM pixels][BN/4 hidden channels] fp32 comes in as whole 16-B chunks of rows, the
+// cell (gate order i, f, g, o: c = f c_prev + i g, h = o tanh c) runs on the MFMA
+// layout (each lane holds the four gates of one hidden channel of one pixel), c and h go
+// back to LDS and leave as whole row chunks (c: BN B per pixel row, h: BN/2 B) instead
+// of one 4-B / 2-B store per lane for 16 scattered pixels.  The gates for the backward
+// keep their direct float4 stores (64 contiguous B per pixel per instruction).
+template <int BM, int BN, int WM, int WN, int NTH>
+STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end,
+                                  int n0, int wm, int wn, int tid, char* smem) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int HC = BN / 4;                            // hidden channels per tile
+  constexpr int PS = HC + 4;                            // fp32 row stride (16-B aligned, skewed)
+  constexpr int CCH = HC / 4, HCH = HC / 8;             // 16-B chunks per c row / h row
+  float* cs = reinterpret_cast<float*>(smem);           // [BM][PS] c_prev, then c
+  bf16* hs = reinterpret_cast<bf16*>(smem + BM * PS * 4);   // [BM][HC + 8] h
+  constexpr int HS = HC + 8;
+  const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
+  const int Ch = a.Nout >> 2, ch0 = n0 >> 2;
+  const int hcn = min(HC, Ch - ch0);                    // hidden channels present in this tile
+  for (int e = tid; e < BM * CCH; e += NTH) {
+    const int r = e / CCH, q = e - r * CCH, m = m0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.c_prev && m < m_end && q * 4 < hcn) v = *reinterpret_cast<const float4*>(a.c_prev + (size_t)m * Ch + ch0 + q * 4);
+    *reinterpret_cast<float4*>(cs + r * PS + q * 4) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WTN + j * 16 + fk * 4, nb = n0 + nl, hl = nl >> 2;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && nb < a.Nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = a.bias[nb + r];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + fr, m = m0 + row;
+      if (!(m < m_end && nb < a.Nout)) continue;
+      const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
+      const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+      const float c = gf * cs[row * PS + hl] + gi * gg;
+      cs[row * PS + hl] = c;
+      hs[row * HS + hl] = f2bf(go * tanhf(c));
+      *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < BM * CCH; e += NTH) {
+    const int r = e / CCH, q = e - r * CCH, m = m0 + r;
+    if (m < m_end && q * 4 < hcn)
+      *reinterpret_cast<float4*>(a.c_out + (size_t)m * Ch + ch0 + q * 4) = *reinterpret_cast<const float4*>(cs + r * PS + q * 4);
+  }
+  const bool hvec = ((reinterpret_cast<uintptr_t>(a.h_out) & 15) == 0) && (a.hcs & 7) == 0;
+  for (int e = tid; e < BM * HCH; e += NTH) {
+    const int r = e / HCH, q = e - r * HCH, m = m0 + r;
+    if (!(m < m_end && q * 8 < hcn)) continue;
+    uint16_t* dst = a.h_out + (size_t)m * a.hcs + ch0 + q * 8;
+    const bf16* src = hs + r * HS + q * 8;
+    if (hvec) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    else
+      for (int k = 0; k < 8; ++k) reinterpret_cast<bf16*>(dst)[k] = src[k];
   }
 }
 
@@ -612,6 +682,9 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   __syncthreads();
   if constexpr (EPI == 0) {
     staged_epilogue<BM, BN, WM, WN, SCATTER, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem, bx, pcls);
+  } else if (EPI == 1 && lstm_staged()) {
+    static_assert(EPI != 1 || LDS_MAIN >= BM * (BN / 4 + 4) * 4 + BM * (BN / 4 + 8) * 2, "LSTM staging");
+    lstm_staged_epilogue<BM, BN, WM, WN, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
   } else {
     int mrow[TM];
 #pragma unroll
