@@ -20,8 +20,11 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/s
   python3 $root/bench.py --model stf > $out/stf_rocprof_bench.json 2> $out/stf.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pk -o run -- \
   python3 $root/tools/bench_pk.py > $out/bench_pk.json 2> $out/pk.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/aug -o run -- \
+  python3 $root/tools/bench_aug.py > $out/aug_rocprof_bench.json 2> $out/aug.log
 cd $root
 timeout -k 10 200 python3 tools/bench_eval.py > $out/bench_eval.txt 2>&1
+timeout -k 10 200 python3 tools/bench_aug.py > $out/bench_aug.json 2> $out/bench_aug.err
 if [ -z "$SKIP_PMC" ]; then
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_unet --steps 3 --warmup 1
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_stf --model stf --steps 3 --warmup 1
@@ -35,5 +38,6 @@ fi
 cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
 cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
 cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
-rm -rf $out/unet $out/stf $out/pk $out/pmc_unet $out/pmc_stf
+cp $out/aug/run_kernel_stats.csv $out/aug_b16_kernel_stats.csv
+rm -rf $out/unet $out/stf $out/pk $out/aug $out/pmc_unet $out/pmc_stf
 ls $out
