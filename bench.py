@@ -184,6 +184,7 @@ def main():
 
     from stfunet import engine, nhwc
     from stfunet.ddp import GradAllReduce
+    from stfunet.flops import stf_train_flops, unet_train_flops
     from stfunet.optim import AdamW
     from stfunet.synthetic import dce_batch
     from stfunet import STFLSTMUNet, UNet
@@ -280,11 +281,9 @@ def main():
     value = samples / elapsed
     if rank == 0:
         if args.model == "unet":
-            from oracle.unet import train_flops_per_sample
-            train_gflop = train_flops_per_sample(args.time_steps, 64, args.size, args.size) / 1e9
+            train_gflop = unet_train_flops(args.time_steps, 64, args.size, args.size) / 1e9
         else:
-            from oracle.stf import train_flops_per_sample
-            train_gflop = train_flops_per_sample(args.time_steps, args.size, args.size, args.pk) / 1e9
+            train_gflop = stf_train_flops(args.time_steps, args.size, args.size, args.pk) / 1e9
         workload = (f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
                     if args.model == "unet" else
                     f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
