@@ -325,7 +325,7 @@ int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W
                        stf_stream_t stream);
 /* nn.LSTM(C, C) weights -> gate-interleaved GEMM operands: wcat [4C][2C] (row
  * 4c+q = torch row q*C+c of [W_ih | W_hh]), wcat_t [2C][4C], bias = b_ih + b_hh
- * interleaved (src/stf_lstm_unet.py:124-127). */
+ * interleaved (src/stf_lstm_unet.py:124-127).  C in {16, 32, ..., 512} (STF_EINVAL otherwise). */
 int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
                   int C, void* wcat, void* wcat_t, float* bias, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */

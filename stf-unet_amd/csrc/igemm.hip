@@ -273,10 +273,21 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
   const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
   const int Ch = a.Nout >> 2, ch0 = n0 >> 2;
   const int hcn = min(HC, Ch - ch0);                    // hidden channels present in this tile
+  // whole 16-B chunks need Ch % 4 (row alignment) and a chunk inside the tile's channels;
+  // a tail chunk (hcn % 4, hcn % 8 for h) moves element by element
+  const bool cvec = (Ch & 3) == 0;
   for (int e = tid; e < BM * CCH; e += NTH) {
     const int r = e / CCH, q = e - r * CCH, m = m0 + r;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.c_prev && m < m_end && q * 4 < hcn) v = *reinterpret_cast<const float4*>(a.c_prev + (size_t)m * Ch + ch0 + q * 4);
+    if (a.c_prev && m < m_end && q * 4 < hcn) {
+      const float* src = a.c_prev + (size_t)m * Ch + ch0 + q * 4;
+      if (cvec && q * 4 + 4 <= hcn) v = *reinterpret_cast<const float4*>(src);
+      else {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < 4 && q * 4 + k < hcn; ++k) t[k] = src[k];
+        v = make_float4(t[0], t[1], t[2], t[3]);
+      }
+    }
     *reinterpret_cast<float4*>(cs + r * PS + q * 4) = v;
   }
   __syncthreads();
@@ -303,8 +314,11 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
   __syncthreads();
   for (int e = tid; e < BM * CCH; e += NTH) {
     const int r = e / CCH, q = e - r * CCH, m = m0 + r;
-    if (m < m_end && q * 4 < hcn)
-      *reinterpret_cast<float4*>(a.c_out + (size_t)m * Ch + ch0 + q * 4) = *reinterpret_cast<const float4*>(cs + r * PS + q * 4);
+    if (!(m < m_end && q * 4 < hcn)) continue;
+    float* dst = a.c_out + (size_t)m * Ch + ch0 + q * 4;
+    if (cvec && q * 4 + 4 <= hcn) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(cs + r * PS + q * 4);
+    else
+      for (int k = 0; k < 4 && q * 4 + k < hcn; ++k) dst[k] = cs[r * PS + q * 4 + k];
   }
   const bool hvec = ((reinterpret_cast<uintptr_t>(a.h_out) & 15) == 0) && (a.hcs & 7) == 0;
   for (int e = tid; e < BM * HCH; e += NTH) {
@@ -312,9 +326,9 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
     if (!(m < m_end && q * 8 < hcn)) continue;
     uint16_t* dst = a.h_out + (size_t)m * a.hcs + ch0 + q * 8;
     const bf16* src = hs + r * HS + q * 8;
-    if (hvec) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    if (hvec && q * 8 + 8 <= hcn) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     else
-      for (int k = 0; k < 8; ++k) reinterpret_cast<bf16*>(dst)[k] = src[k];
+      for (int k = 0; k < 8 && q * 8 + k < hcn; ++k) reinterpret_cast<bf16*>(dst)[k] = src[k];
   }
 }
 

@@ -297,7 +297,10 @@ extern "C" int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, i
 
 extern "C" int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, int C,
                              void* wcat, void* wcat_t, float* bias, stf_stream_t stream) {
-  if (C % 8) return STF_EINVAL;
+  // the step GEMM's K = 2C rows stream in 32-channel steps (no masked K tail on the
+  // LSTM epilogue path) and the bias gradient's channel sum wants 4C / 8 | 256:
+  // hidden sizes 16, 32, ..., 512 (the reference's are 64..512)
+  if (C < 16 || C % 16 || 512 % C) return STF_EINVAL;
   hipLaunchKernelGGL(lstm_pack_kernel, dim3(grid_for(8L * C * C, 4096)), dim3(NT), 0, (hipStream_t)stream, w_ih,
                      w_hh, b_ih, b_hh, C, (bf16*)wcat, (bf16*)wcat_t, bias);
   STF_CHECK_LAUNCH();

@@ -14,10 +14,17 @@ reference's order: RandomResize ``randint``, two flip ``random()``, rotation
 nearest-neighbour index tables and the rotation matrix.  One descriptor per frame goes
 to the device with the sources (one uint8 arena, one copy).
 
-``paired=True`` (default) draws ONE parameter set per sample for all its frames, PK
-maps and its mask -- the alignment the reference intends; ``paired=False`` reproduces
-the reference's behaviour, a fresh draw per frame (frame 0 shares the mask's draw,
-my_dataset.py:211-218, PK maps draw their own, :233-237).  No CPU fallback.
+``paired=False`` (default) reproduces the reference's behaviour: a fresh draw per
+frame (frame 0 shares the mask's draw, my_dataset.py:211-218, PK maps draw their own,
+:233-237), so loss / Dice curves are comparable with the reference's.  ``paired=True``
+(opt-in fix) draws ONE parameter set per sample for all its frames, PK maps and its
+mask -- the alignment the reference intends but does not implement.  No CPU fallback.
+
+Random stream: ``seed=None`` draws from the global ``random`` module at draw time (as
+the reference does; torch reseeds it in every DataLoader worker).  With a seed, a
+private ``random.Random`` is used; inside a DataLoader worker it is re-created from
+(seed, worker id, worker seed) on first use, so workers never replay one another's
+parameter stream.
 """
 import ctypes
 import math
@@ -118,15 +125,27 @@ class DeviceAugment:
     (x fp32 [B][F][1][oh][ow], target int64 [B][oh][ow]) on the device."""
 
     def __init__(self, train=True, base_size=256, crop_size=224, mean=MEAN, std=STD, hflip_prob=0.5,
-                 vflip_prob=0.5, degrees=30, paired=True, seed=None, device=None):
+                 vflip_prob=0.5, degrees=30, paired=False, seed=None, device=None):
         self.train, self.base, self.crop = train, base_size, crop_size
         self.mean, self.std = float(mean), float(std)
         self.hflip_prob, self.vflip_prob, self.degrees = hflip_prob, vflip_prob, degrees
         self.paired = paired
-        # seed None: the global ``random`` module, as the reference draws (DataLoader
-        # workers reseed it per worker); else a private generator
-        self.rng = random.Random(seed) if seed is not None else random
+        self.seed = seed
+        self._rng, self._rng_owner = None, None     # owner: worker id the generator belongs to
         self.device = torch.device(device) if device is not None else torch.device("cuda")
+
+    @property
+    def rng(self):
+        """The generator draws come from (see the module docstring).  Never the module
+        object itself is stored, so the instance pickles for spawn / forkserver workers."""
+        if self.seed is None:
+            return random
+        info = torch.utils.data.get_worker_info()
+        owner = None if info is None else info.id
+        if self._rng is None or self._rng_owner != owner:
+            key = self.seed if info is None else hash((self.seed, info.id, info.seed))
+            self._rng, self._rng_owner = random.Random(key), owner
+        return self._rng
 
     # ------------------------------------------------------------- draws (train.py:58-63 order)
     def draw(self, h, w):

@@ -82,8 +82,22 @@ def test_draw_order_matches_reference_sequence():
         got = aug.draw_sample(4, h, w)
         want = [A.draw_train(r, h, w) for _ in range(4)]
         assert got == want
-    paired = G.DeviceAugment(train=True, seed=3, device="cpu").draw_sample(8, 256, 256)
+    paired = G.DeviceAugment(train=True, seed=3, device="cpu", paired=True).draw_sample(8, 256, 256)
     assert all(p is paired[0] for p in paired)
+    default = G.DeviceAugment(train=True, seed=3, device="cpu").draw_sample(8, 256, 256)
+    assert len({repr(p) for p in default}) > 1                  # reference default: a draw per frame
+
+
+def test_unseeded_augment_pickles():
+    """seed=None keeps no module reference: picklable for spawn / forkserver workers."""
+    import pickle
+    from stfunet import augment as G
+    aug = pickle.loads(pickle.dumps(G.DeviceAugment(train=True, device="cpu")))
+    assert aug.rng is random
+    seeded = G.DeviceAugment(train=True, seed=4, device="cpu")
+    seeded.draw(64, 64)
+    twin = pickle.loads(pickle.dumps(seeded))
+    assert twin.draw(64, 64) == seeded.draw(64, 64)
 
 
 def test_eval_size_rule():

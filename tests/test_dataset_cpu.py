@@ -43,3 +43,26 @@ def test_rejects_foreign_transforms(tmp_path):
     make_tree(str(tmp_path))
     with pytest.raises(TypeError):
         DriveDataset(str(tmp_path), "train", transforms=lambda a, b: (a, b))
+
+
+def _identity(batch):
+    return batch
+
+
+def test_seeded_workers_draw_different_streams(tmp_path):
+    """Each DataLoader worker re-creates the seeded generator from (seed, worker id,
+    worker seed): two workers never replay the same parameter stream, and a run with the
+    same torch seed reproduces the same draws."""
+    from stfunet.augment import DeviceAugment
+    from stfunet.dataset import DriveDataset
+    make_tree(str(tmp_path))
+    ds = DriveDataset(str(tmp_path), "train", transforms=DeviceAugment(seed=5, device="cpu"))
+
+    def run():
+        torch.manual_seed(0)
+        loader = torch.utils.data.DataLoader(ds, batch_size=1, num_workers=2, collate_fn=_identity)
+        return [b[0][2] for b in loader]
+    params = run()
+    assert len(params) >= 2
+    assert params[0] != params[1]                        # worker 0 vs worker 1, first draw each
+    assert run() == params

@@ -130,9 +130,11 @@ def test_basic_block_grouped_bn(cin, cout, stride, groups):
             assert int(b) == int(br) == groups, name
 
 
-@pytest.mark.parametrize("C,T", [(64, 3), (128, 2)])
+@pytest.mark.parametrize("C,T", [(64, 3), (128, 2), (16, 3), (32, 2)])
 def test_lstm_component(C, T):
-    """Per-pixel nn.LSTM over T (only h_T used) vs torch nn.LSTM."""
+    """Per-pixel nn.LSTM over T (only h_T used) vs torch nn.LSTM.  C = 16: a hidden size
+    that fills only part of a GEMM tile's hidden channels (the staged epilogue's chunk
+    bounds); stf_lstm_pack rejects sizes outside {16, 32, ..., 512}."""
     from stfunet import nhwc
     from stfunet.stf_lstm_unet import LSTMProgram
     lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
@@ -161,6 +163,17 @@ def test_lstm_component(C, T):
     assert rel(dx_t, xr.grad.permute(1, 0, 2)) < 4e-2
     for name, p in lstm.named_parameters():
         assert rel(gv(p), p.grad) < 4e-2, name
+
+
+def test_lstm_rejects_unsupported_hidden_size():
+    from stfunet.stf_lstm_unet import LSTMProgram
+    from stfunet import nhwc
+    from stfunet._lib import HipError
+    C = 48
+    lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
+    lbuf = nhwc.zeros_feat(2 * 2, 4, 4, 2 * C, DEV)
+    with pytest.raises(HipError):
+        LSTMProgram(lstm).forward(lbuf, 2, 2, nhwc.new_feat(2, 4, 4, C, DEV))
 
 
 def test_maxpool3_fwd_bwd():
