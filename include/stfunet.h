@@ -53,11 +53,23 @@ typedef struct stf_conv_geom {
  * the epilogue adds the bias and applies c_t = f*c_{t-1} + i*g, h_t = o*tanh(c_t)
  * (nn.LSTM, src/stf_lstm_unet.py:124-127,219-235). */
 typedef struct stf_lstm_epi {
-  const float* c_prev; /* [M][Ch] or NULL (zero initial state)                    */
-  float* c_out;        /* [M][Ch]                                                 */
+  const float* c_prev; /* [M][Ch] c_{t-1}, or NULL (zero initial state)           */
+  float* c_out;        /* forward: c_t out [M][Ch]; backward: c_t in (read only)  */
   void* h_out;         /* bf16, h_t written with stride h_cstride (may be the next */
   int h_cstride;       /* step's [x | h] buffer or the decoder's concat slice)     */
-  float* gates;        /* [M][4Ch] activated gates (i, f, g, o), for backward     */
+  float* gates;        /* forward: [M][4Ch] activated gates (i, f, g, o), or NULL  */
+                       /* when the backward recomputes them (backward = 1)        */
+  /* backward = 1: the GEMM recomputes step t's gate pre-activations from the same
+   * [x_t | h_{t-1}] rows and weights (same kernel, so bitwise the forward's gates)
+   * and the epilogue runs the cell backward (h_out / gates unused):
+   *   tc = tanh c_t; dc = dh*o*(1-tc^2) + dc_next; dc_prev = dc*f;
+   *   dgates = (dc*g*i(1-i), dc*c_{t-1}*f(1-f), dc*i*(1-g^2), dh*tc*o(1-o)) */
+  int backward;
+  const void* dh;      /* bf16 dL/dh_t, stride dh_cstride                          */
+  int dh_cstride;
+  const float* dc_next;/* [M][Ch] dL/dc_t from step t+1, or NULL (t = T-1)          */
+  float* dc_prev;      /* [M][Ch] out, dL/dc_{t-1} (may alias dc_next)              */
+  void* dgates;        /* bf16 [M][4Ch] pre-activation gate gradients, interleaved */
 } stf_lstm_epi;
 
 /* BatchNorm-backward reduction fused into a dgrad: dst receives dz, the gradient

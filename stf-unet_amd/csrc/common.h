@@ -38,6 +38,13 @@ STF_DEV uint4 pack8(const float (&f)[8]) {
 
 STF_DEV float round_bf(float v) { return bf2f(f2bf(v)); }
 
+// LSTM activations on the hardware transcendental units (v_exp_f32, v_rcp_f32): ~1e-7
+// absolute error, far below the bf16 storage of h.  The forward cell, the backward's
+// gate recompute and the cell backward all use these, so the recomputed gates equal
+// the forward's bit for bit.
+STF_DEV float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+STF_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
+
 // ---------------------------------------------------------------- reductions
 STF_DEV float wave_sum(float v) {
 #pragma unroll

@@ -30,6 +30,8 @@ struct Geo {
   int accumulate;
   // LSTM cell epilogue (Nout = 4*Ch, column 4c+q = gate q of hidden channel c)
   const float* c_prev; float* c_out; uint16_t* h_out; int hcs; float* gates;
+  // LSTM cell backward epilogue (EPI 2, gates recomputed): c_out = c_t (read)
+  const uint16_t* l_dh; int l_dhcs; const float* l_dcn; float* l_dcp; uint16_t* l_dg;
   // fused BN-backward reduction (stf_bnr_epi)
   const uint16_t* bnr_y; int bnr_ycs; const float *bnr_scale, *bnr_shift, *bnr_mean, *bnr_invstd;
   int bnr_relu; float* bnr_part;
@@ -42,7 +44,7 @@ struct Geo {
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
 
-STF_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
 
 #ifndef STF_LSTM_STAGED
 #define STF_LSTM_STAGED 1
@@ -78,12 +80,31 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
         // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
         const int ch = nb >> 2, Ch = a.Nout >> 2;
         const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-        const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+        const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
         const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
         const float c = gf * cp + gi * gg;
         a.c_out[(size_t)m * Ch + ch] = c;
-        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanhf(c));
-        *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanh_f(c));
+        if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+        continue;
+      }
+      if (EPI == 2) {
+        // LSTM cell backward on the recomputed gates (the forward's arithmetic, same GEMM):
+        // dc = dh*o*(1-tanh(c)^2) + dc_next, dc_prev = dc*f, pre-activation gate gradients
+        const int ch = nb >> 2, Ch = a.Nout >> 2;
+        const size_t u = (size_t)m * Ch + ch;
+        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
+        const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+        const float tc = tanh_f(a.c_out[u]);
+        const float h = bf2f(reinterpret_cast<const bf16*>(a.l_dh)[(size_t)m * a.l_dhcs + ch]);
+        const float dc = h * go * (1.f - tc * tc) + (a.l_dcn ? a.l_dcn[u] : 0.f);
+        const float cp = a.c_prev ? a.c_prev[u] : 0.f;
+        const float d_o = h * tc * go * (1.f - go);
+        const float d_i = dc * gg * gi * (1.f - gi);
+        const float d_g = dc * gi * (1.f - gg * gg);
+        const float d_f = dc * cp * gf * (1.f - gf);
+        a.l_dcp[u] = dc * gf;
+        *reinterpret_cast<uint2*>(a.l_dg + (size_t)m * a.Nout + nb) = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
         continue;
       }
       float v[4];
@@ -304,11 +325,11 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
       const int row = wm * WTM + i * 16 + fr, m = m0 + row;
       if (!(m < m_end && nb < a.Nout)) continue;
       const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-      const float gg = tanhf(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+      const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
       const float c = gf * cs[row * PS + hl] + gi * gg;
       cs[row * PS + hl] = c;
-      hs[row * HS + hl] = f2bf(go * tanhf(c));
-      *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
+      hs[row * HS + hl] = f2bf(go * tanh_f(c));
+      if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
     }
   }
   __syncthreads();
@@ -329,6 +350,96 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
     if (hvec && q * 8 + 8 <= hcn) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     else
       for (int k = 0; k < 8 && q * 8 + k < hcn; ++k) reinterpret_cast<bf16*>(dst)[k] = src[k];
+  }
+}
+
+// LSTM cell-backward epilogue (EPI 2), staged through LDS like the forward's: the
+// block's c_t, c_{t-1}, dc_next (fp32) and dh (bf16) tiles come in as whole 16-B row
+// chunks, the cell backward runs on the MFMA layout (a lane holds the four recomputed
+// gate pre-activations of one hidden channel of one pixel), dc_prev goes back to LDS
+// (over dc_next) and leaves as row chunks; the four bf16 gate gradients of a lane are
+// one 8-B store (32 contiguous bytes per pixel per wave-instruction).
+template <int BM, int BN>
+constexpr int lstm_bwd_lds() { return 3 * BM * (BN / 4 + 4) * 4 + BM * (BN / 4 + 8) * 2; }
+
+template <int BM, int BN, int WM, int WN, int NTH>
+STF_DEV void lstm_bwd_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], int m0, int m_end,
+                                      int n0, int wm, int wn, int tid, char* smem) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int HC = BN / 4, PS = HC + 4, HS = HC + 8, CCH = HC / 4, HCH = HC / 8;
+  float* cts = reinterpret_cast<float*>(smem);           // [BM][PS] c_t
+  float* cps = cts + BM * PS;                            // [BM][PS] c_{t-1}
+  float* dcs = cps + BM * PS;                            // [BM][PS] dc_next, then dc_prev
+  bf16* dhs = reinterpret_cast<bf16*>(dcs + BM * PS);    // [BM][HS] dh
+  const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
+  const int Ch = a.Nout >> 2, ch0 = n0 >> 2;
+  const int hcn = min(HC, Ch - ch0);
+  const bool cvec = (Ch & 3) == 0;
+  auto ld4 = [&](const float* base, int m, int q) {
+    if (!base || m >= m_end || q * 4 >= hcn) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* src = base + (size_t)m * Ch + ch0 + q * 4;
+    if (cvec && q * 4 + 4 <= hcn) return *reinterpret_cast<const float4*>(src);
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 4 && q * 4 + k < hcn; ++k) t[k] = src[k];
+    return make_float4(t[0], t[1], t[2], t[3]);
+  };
+  for (int e = tid; e < BM * CCH; e += NTH) {
+    const int r = e / CCH, q = e - r * CCH, m = m0 + r;
+    *reinterpret_cast<float4*>(cts + r * PS + q * 4) = ld4(a.c_out, m, q);
+    *reinterpret_cast<float4*>(cps + r * PS + q * 4) = ld4(a.c_prev, m, q);
+    *reinterpret_cast<float4*>(dcs + r * PS + q * 4) = ld4(a.l_dcn, m, q);
+  }
+  const bool hvec = ((reinterpret_cast<uintptr_t>(a.l_dh) & 15) == 0) && (a.l_dhcs & 7) == 0;
+  for (int e = tid; e < BM * HCH; e += NTH) {
+    const int r = e / HCH, q = e - r * HCH, m = m0 + r;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (m < m_end && q * 8 < hcn) {
+      const uint16_t* src = a.l_dh + (size_t)m * a.l_dhcs + ch0 + q * 8;
+      if (hvec && q * 8 + 8 <= hcn) v = *reinterpret_cast<const uint4*>(src);
+      else {
+        uint16_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < 8 && q * 8 + k < hcn; ++k) t[k] = src[k];
+        v = make_uint4(t[0] | ((uint32_t)t[1] << 16), t[2] | ((uint32_t)t[3] << 16), t[4] | ((uint32_t)t[5] << 16),
+                       t[6] | ((uint32_t)t[7] << 16));
+      }
+    }
+    *reinterpret_cast<uint4*>(dhs + r * HS + q * 8) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WTN + j * 16 + fk * 4, nb = n0 + nl, hl = nl >> 2;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias && nb < a.Nout) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = a.bias[nb + r];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + fr, m = m0 + row;
+      if (!(m < m_end && nb < a.Nout)) continue;
+      const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
+      const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
+      const float tc = tanh_f(cts[row * PS + hl]);
+      const float h = bf2f(dhs[row * HS + hl]);
+      const float dc = h * go * (1.f - tc * tc) + dcs[row * PS + hl];
+      const float cp = cps[row * PS + hl];
+      const float d_o = h * tc * go * (1.f - go);
+      const float d_i = dc * gg * gi * (1.f - gi);
+      const float d_g = dc * gi * (1.f - gg * gg);
+      const float d_f = dc * cp * gf * (1.f - gf);
+      dcs[row * PS + hl] = dc * gf;
+      *reinterpret_cast<uint2*>(a.l_dg + (size_t)m * a.Nout + nb) = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < BM * CCH; e += NTH) {
+    const int r = e / CCH, q = e - r * CCH, m = m0 + r;
+    if (!(m < m_end && q * 4 < hcn)) continue;
+    float* dst = a.l_dcp + (size_t)m * Ch + ch0 + q * 4;
+    if (cvec && q * 4 + 4 <= hcn) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(dcs + r * PS + q * 4);
+    else
+      for (int k = 0; k < 4 && q * 4 + k < hcn; ++k) dst[k] = dcs[r * PS + q * 4 + k];
   }
 }
 
@@ -506,7 +617,7 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   constexpr int LA = BM / NW / RPI, LB = BN / NW / RPI; // DMA instructions per wave per K step
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int LDS_MAIN = STAGES * STAGE;
-  constexpr int LDS_RED = EPI == 0 ? BM * BN * 2 + NW * 2 * BN * 4 : WM * 2 * BN * 4;
+  constexpr int LDS_RED = EPI == 0 ? BM * BN * 2 + NW * 2 * BN * 4 : (EPI == 2 ? lstm_bwd_lds<BM, BN>() : WM * 2 * BN * 4);
   static_assert(LA >= 1 && LB >= 1 && LA * RPI * NW == BM && LB * RPI * NW == BN, "tile");
   __shared__ __attribute__((aligned(16))) char smem[LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED];
 
@@ -699,6 +810,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
   } else if (EPI == 1 && lstm_staged()) {
     static_assert(EPI != 1 || LDS_MAIN >= BM * (BN / 4 + 4) * 4 + BM * (BN / 4 + 8) * 2, "LSTM staging");
     lstm_staged_epilogue<BM, BN, WM, WN, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
+  } else if (EPI == 2 && lstm_staged()) {
+    lstm_bwd_staged_epilogue<BM, BN, WM, WN, NTH>(a, acc, m0, m_end, n0, wm, wn, tid, smem);
   } else {
     int mrow[TM];
 #pragma unroll
@@ -1358,6 +1471,14 @@ char forced_cfg() {
   return c;
 }
 
+char lstm_forced_cfg() {
+  static const char c = [] {
+    const char* e = getenv("STF_LSTM_CFG");
+    return (e && (e[0] == 'A' || e[0] == 'B' || e[0] == 'C' || e[0] == 'D')) ? e[0] : '\0';
+  }();
+  return c;
+}
+
 // STF_IGEMM_DMA=0 selects the register-staged kernel (A/B comparisons); read once.
 bool dma_enabled() {
   static const bool on = [] {
@@ -1376,6 +1497,16 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   if (!dma_enabled() || !dma_ok || c.Cs % 32) return 'R';
   const char f = forced_cfg();
   const bool bk64 = c.Cs % 64 == 0;
+  if (a->lstm) {
+    // LSTM steps (1x1 GEMM, K = 2C): per-scale tile (STF_LSTM_CFG forces one, A/B);
+    // any tile gives the same gates (same MFMA sequence over ascending K), so the
+    // backward recompute may run a different tile than the forward
+    const char lf = lstm_forced_cfg();
+    char k = lf ? lf : 'A';
+    if (!bk64 && k != 'A') k = 'A';
+    if (k == 'C' && a->lstm->backward) k = 'B';     // the 256x256 tile has no room for the bwd staging
+    return k;
+  }
   const bool halo_ok = plain && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs &&
                        c.Wd == c.Ws && a->Nout % 64 == 0;
   if (f == 'H' && halo_ok) return 'H';
@@ -1413,13 +1544,14 @@ Cfg cfg_of(char k) {
 }
 
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
-void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, bool c8, uint32_t src_bytes, hipStream_t s) {
+void launch_dma(const Geo& g, bool trans, bool scatter, int lstm, bool c8, uint32_t src_bytes, hipStream_t s) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN, g.ksplit), block(64 * WM * WN);
 #define STF_D(TR, SCA, E) \
   hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, TR, SCA, E>), grid, block, 0, s, g, src_bytes)
   if (c8)
     hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 0, true>), grid, block, 0, s, g,
                        src_bytes);
+  else if (lstm == 2) STF_D(false, false, 2);
   else if (lstm) STF_D(false, false, 1);
   else if (scatter) STF_D(false, true, 0);
   else if (trans) STF_D(true, false, 0);
@@ -1427,11 +1559,22 @@ void launch_dma(const Geo& g, bool trans, bool scatter, bool lstm, bool c8, uint
 #undef STF_D
 }
 
-// plain forward gather (or its ConvT 2x2 scatter epilogue) on the 8-wave tiles
+// plain forward gather (or its ConvT 2x2 scatter epilogue, or an LSTM step: lstm 1 =
+// cell, 2 = cell backward) on the 8-wave tiles
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES>
-void launch_dma_plain(const Geo& g, bool scatter, uint32_t src_bytes, hipStream_t s) {
+void launch_dma_plain(const Geo& g, bool scatter, uint32_t src_bytes, hipStream_t s, int lstm = 0) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN, g.ksplit), block(64 * WM * WN);
-  if (scatter)
+  if constexpr (lstm_bwd_lds<BM, BN>() <= 163840) {
+    if (lstm == 2) {
+      hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 2>), grid, block, 0, s, g,
+                         src_bytes);
+      return;
+    }
+  }
+  if (lstm)
+    hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, false, 1>), grid, block, 0, s, g,
+                       src_bytes);
+  else if (scatter)
     hipLaunchKernelGGL((igemm_dma_kernel<BM, BN, WM, WN, BKK, STAGES, false, true, 0>), grid, block, 0, s, g,
                        src_bytes);
   else
@@ -1440,10 +1583,14 @@ void launch_dma_plain(const Geo& g, bool scatter, uint32_t src_bytes, hipStream_
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch_reg(const Geo& g, bool smallc, bool trans, bool scatter, bool lstm, hipStream_t s) {
+int launch_reg(const Geo& g, bool smallc, bool trans, bool scatter, int lstm, hipStream_t s) {
   dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + BN - 1) / BN), block(NT);
 #define STF_L(SC, TR, SCA, E) hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, SC, TR, SCA, E>), grid, block, 0, s, g)
-  if (lstm) { if (smallc) return STF_EINVAL; STF_L(false, false, false, 1); }
+  if (lstm) {
+    if (smallc) return STF_EINVAL;
+    if (lstm == 2) STF_L(false, false, false, 2);
+    else STF_L(false, false, false, 1);
+  }
   else if (scatter) { if (smallc) STF_L(true, false, true, 0); else STF_L(false, false, true, 0); }
   else if (trans) { if (smallc) STF_L(true, true, false, 0); else STF_L(false, true, false, 0); }
   else { if (smallc) STF_L(true, false, false, 0); else STF_L(false, false, false, 0); }
@@ -1536,7 +1683,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   static thread_local char buf[128];
   const stf_conv_geom& c = a->g;
   const char k = choose(a, dma_fits(a));
-  const int epi = a->lstm ? 1 : 0;
+  const int epi = a->lstm ? (a->lstm->backward ? 2 : 1) : 0;
   const char* tr = c.transposed ? "true" : "false";
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
@@ -1550,9 +1697,9 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
     case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
     case 'a': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, false, false, 0, true>"); break;
     case 'e': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, false, false, 0, true>"); break;
-    case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, 0, false>", sc); break;
-    case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, 0, false>", sc); break;
-    case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, 0, false>", sc); break;
+    case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, %d, false>", sc, epi); break;
+    case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, %d, false>", sc, epi); break;
+    case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, %d, false>", sc, epi); break;
     default: {
       const bool small = (a->Nout <= 64 && !a->lstm);
       snprintf(buf, sizeof buf, "igemm_kernel<%s, %s, %s, %s, %d>", small ? "256, 64, 4, 1" : "128, 128, 2, 2",
@@ -1608,11 +1755,22 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
     g.bnr_invstd = a->bnr->invstd; g.bnr_relu = a->bnr->relu; g.bnr_part = a->bnr->partial;
   }
+  g.l_dh = nullptr; g.l_dhcs = 0; g.l_dcn = nullptr; g.l_dcp = nullptr; g.l_dg = nullptr;
+  int lstm_epi = 0;
   if (a->lstm) {
-    if (a->scatter2x2 || c.transposed || a->Nout % 4 || !a->lstm->c_out || !a->lstm->h_out || !a->lstm->gates)
-      return STF_EINVAL;
-    g.c_prev = a->lstm->c_prev; g.c_out = a->lstm->c_out; g.h_out = (uint16_t*)a->lstm->h_out;
-    g.hcs = a->lstm->h_cstride; g.gates = a->lstm->gates;
+    const stf_lstm_epi& l = *a->lstm;
+    if (a->scatter2x2 || c.transposed || a->Nout % 4 || !l.c_out) return STF_EINVAL;
+    if (l.backward) {
+      if (!l.dh || !l.dc_prev || !l.dgates || ((uintptr_t)l.dgates & 7)) return STF_EINVAL;
+      g.l_dh = (const uint16_t*)l.dh; g.l_dhcs = l.dh_cstride; g.l_dcn = l.dc_next; g.l_dcp = l.dc_prev;
+      g.l_dg = (uint16_t*)l.dgates;
+      lstm_epi = 2;
+    } else {
+      if (!l.h_out) return STF_EINVAL;
+      lstm_epi = 1;
+    }
+    g.c_prev = l.c_prev; g.c_out = l.c_out; g.h_out = (uint16_t*)l.h_out;
+    g.hcs = l.h_cstride; g.gates = l.gates;
   }
   const bool smallc = (c.Cs % BK) != 0;
   hipStream_t s = (hipStream_t)stream;
@@ -1678,16 +1836,16 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     g.ksplit = ks; g.ws = a->ws;
   }
   switch (k) {
-    case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
-    case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, a->lstm, false, src_bytes, s); break;
+    case 'A': launch_dma<128, 128, 2, 2, 32, 4>(g, c.transposed, a->scatter2x2, lstm_epi, false, src_bytes, s); break;
+    case 'E': launch_dma<256, 64, 4, 1, 32, 4>(g, c.transposed, a->scatter2x2, lstm_epi, false, src_bytes, s); break;
     case 'a': launch_dma<128, 128, 2, 2, 32, 4>(g, false, false, false, true, src_bytes, s); break;
     case 'e': launch_dma<256, 64, 4, 1, 32, 4>(g, false, false, false, true, src_bytes, s); break;
-    case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, a->scatter2x2, src_bytes, s); break;
-    case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, a->scatter2x2, src_bytes, s); break;
-    case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, a->scatter2x2, src_bytes, s); break;
+    case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
+    case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
+    case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
     default:
-      if (bm == 256) return launch_reg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
-      return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, a->lstm, s);
+      if (bm == 256) return launch_reg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, lstm_epi, s);
+      return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, lstm_epi, s);
   }
   STF_CHECK_LAUNCH();
   if (g.ksplit > 1) {

@@ -336,4 +336,4 @@ extern "C" const char* stf_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-extern "C" int stf_abi_version(void) { return 5; }
+extern "C" int stf_abi_version(void) { return 6; }

@@ -207,7 +207,7 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
     const float4 gv = *reinterpret_cast<const float4*>(gates + m * 4 * C + 4 * c);
     const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
     const float ct = cst[u];
-    const float tc = tanhf(ct);
+    const float tc = tanh_f(ct);
     const float h = bf2f(reinterpret_cast<const bf16*>(dh)[m * dhcs + c]);
     float dc = h * go * (1.f - tc * tc) + (dc_in ? dc_in[u] : 0.f);
     const float cp = cprev ? cprev[u] : 0.f;

@@ -26,7 +26,9 @@ class ConvGeom(ctypes.Structure):
 
 
 class LstmEpi(ctypes.Structure):
-    _fields_ = [("c_prev", P), ("c_out", P), ("h_out", P), ("h_cstride", c_int), ("gates", P)]
+    _fields_ = [("c_prev", P), ("c_out", P), ("h_out", P), ("h_cstride", c_int), ("gates", P),
+                ("backward", c_int), ("dh", P), ("dh_cstride", c_int), ("dc_next", P), ("dc_prev", P),
+                ("dgates", P)]
 
 
 class BnrEpi(ctypes.Structure):

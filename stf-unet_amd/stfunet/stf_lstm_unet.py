@@ -172,7 +172,10 @@ class LSTMProgram:
     ``lbuf``: [T*B images][h][w][2C] with rows of step t = [x_t | h_{t-1}] (x_t written
     by the encoder, h_{-1} = 0).  Step t is one implicit GEMM (K = 2C, N = 4C
     gate-interleaved) with the cell update in its epilogue; h_t lands in step t+1's
-    rows and h_T in ``hT`` (e.g. the decoder's concat slice).
+    rows and h_T in ``hT`` (e.g. the decoder's concat slice).  Only the cell states
+    c_t (fp32) are kept for the backward: each backward step reruns step t's GEMM on
+    the same rows (same kernel, bitwise the forward's gates) with the cell backward in
+    its epilogue, instead of storing T x P x 4C fp32 activated gates.
     """
 
     def __init__(self, lstm):
@@ -188,15 +191,14 @@ class LSTMProgram:
         bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
         call("stf_lstm_pack", _p(L.weight_ih_l0.detach()), _p(L.weight_hh_l0.detach()), _p(L.bias_ih_l0.detach()),
              _p(L.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias), stream())
-        gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev)
         cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
         for t in range(T):
             src = rows(lbuf, t * B, B)
             hdst = rows(lbuf, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
-            epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, _p(gates[t]))
+            epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, None)
             nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
         st = _S()
-        st.lbuf, st.T, st.B, st.wcat_t, st.gates, st.c = lbuf, T, B, wcat_t, gates, cst
+        st.lbuf, st.T, st.B, st.wcat, st.wcat_t, st.bias, st.c = lbuf, T, B, wcat, wcat_t, bias, cst
         return st
 
     def backward(self, st, dhT: Feat, gv):
@@ -210,8 +212,11 @@ class LSTMProgram:
         for t in range(T - 1, -1, -1):
             dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
             dgt = rows(dg, t * B, B)
-            call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None, dh.ptr(),
-                 dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
+            src = rows(lb, t * B, B)
+            # recompute step t's gates (same GEMM as the forward) + cell backward epilogue
+            epi = LstmEpi(_p(st.c[t - 1]) if t > 0 else None, _p(st.c[t]), None, 0, None,
+                          1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
+            nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
             nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
         dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
         nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat)

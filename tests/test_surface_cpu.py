@@ -47,7 +47,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
     assert set(syms) == set(_lib.EXPORTED)
-    assert lib.stf_abi_version() == 5
+    assert lib.stf_abi_version() == 6
     assert b"invalid argument" in lib.stf_error_string(100001)
 
 
