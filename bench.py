@@ -31,7 +31,7 @@ sys.path.insert(0, HERE)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2500.0     # MI355X dense bf16 = fp16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -40,12 +40,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)      # >= 50 timed after >= 10 warm-up
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="BASELINE.json configs[k-1] preset: 2 = UNet 256^2 B64 bf16 (the default workload), "
+                         "3 = STF T8 256^2 B16 bf16, 4 = STF T16 256^2 B16 per GPU bf16 (the 8-GPU DDP config), "
+                         "5 = STF T32+3 PK 512^2 fp16 + GradScaler, B4 per GPU")
     ap.add_argument("--model", default="unet", choices=["unet", "stf"],
                     help="unet = BASELINE configs[1] (default); stf = configs[2] (T=8, B=16)")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (unet 64, stf 16)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--time-steps", type=int, default=8)
     ap.add_argument("--pk", action="store_true", help="STF with 3 PK-map channels (configs[4])")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="16-bit activation storage; fp16 = the reference's --amp step (autocast float16 + "
+                         "GradScaler, train_and_eval.py:389-404) on the fp16 library")
     ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
                     help="replay the training step as a HIP graph (N=1 only; auto = STF).  Off by default: "
                          "measured slower than eager for STF (12.92 vs 12.49 ms/step), the replay loses most "
@@ -53,7 +60,26 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timer", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    presets = {2: dict(model="unet", batch=64, size=256, time_steps=8, pk=False, dtype="bf16"),
+               3: dict(model="stf", batch=16, size=256, time_steps=8, pk=False, dtype="bf16"),
+               4: dict(model="stf", batch=16, size=256, time_steps=16, pk=False, dtype="bf16"),
+               5: dict(model="stf", batch=4, size=512, time_steps=32, pk=True, dtype="fp16")}
+    if a.config is not None:
+        for k, v in presets[a.config].items():
+            if k != "batch" or a.batch is None:          # an explicit --batch wins
+                setattr(a, k, v)
+    return a
+
+
+def workload_name(args):
+    if args.model == "unet":
+        cfg = "cfg2" if (args.size, args.time_steps) == (256, 8) else "custom"
+        return f"{cfg} UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
+    cfg = {(256, 8, False): "cfg3", (256, 16, False): "cfg4 (per GPU)", (512, 32, True): "cfg5 (per GPU)"}.get(
+        (args.size, args.time_steps, args.pk), "custom")
+    return (f"{cfg} STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) {args.size}x{args.size} "
+            f"train step")
 
 
 def pmc_traffic(kernel, workload, batch):
@@ -125,7 +151,7 @@ def cpu_baseline(args):
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores = max(1, min(cores, 16))
     torch.set_num_threads(cores)
-    b = 2
+    b = 2 if args.size <= 256 else 1           # bounded sample (~10-30 s of CPU work)
     g = torch.Generator().manual_seed(1)
     if args.model == "unet":
         sd = canonical_state_dict(o_unet.template_state_dict(args.time_steps, 2, 64), seed=0)
@@ -197,7 +223,12 @@ def main():
     else:
         model = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=args.time_steps, use_pk_maps=args.pk).to(dev)
     model.train()
+    fp16 = args.dtype == "fp16"
+    model.storage_dtype = torch.float16 if fp16 else torch.bfloat16
+    scaler = torch.amp.GradScaler("cuda") if fp16 else None
     use_graph = args.graph == "on" or (args.graph == "auto" and args.model == "stf" and world == 1)
+    if use_graph and fp16:
+        raise SystemExit("--graph on runs the bf16 step only (GradScaler's inf check syncs the host)")
     if use_graph and world > 1:
         raise SystemExit("--graph on needs N=1 (RCCL gradient buckets are not captured)")
     opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8,
@@ -213,13 +244,22 @@ def main():
     batches = [(engine.preprocess_input(x, model), t) for x, t in batches]
 
     def train_step(i):
+        # train_one_epoch's step (train_and_eval.py:384-409); fp16 = its --amp branch
         x, t = batches[i % len(batches)]
-        loss = engine.criterion(model(x), t)
+        with torch.amp.autocast(device_type="cuda", enabled=fp16):
+            loss = engine.criterion(model(x), t)
         opt.zero_grad()
-        loss.backward()
-        if ddp is not None:
-            ddp.finish()
-        opt.step()
+        if scaler is not None:
+            scaler.scale(loss).backward()
+            if ddp is not None:
+                ddp.finish()
+            scaler.step(opt)
+            scaler.update()
+        else:
+            loss.backward()
+            if ddp is not None:
+                ddp.finish()
+            opt.step()
         sched.step()
         return loss
 
@@ -284,10 +324,7 @@ def main():
             train_gflop = unet_train_flops(args.time_steps, 64, args.size, args.size) / 1e9
         else:
             train_gflop = stf_train_flops(args.time_steps, args.size, args.size, args.pk) / 1e9
-        workload = (f"cfg2 UNet(in={args.time_steps},base_c=64) {args.size}x{args.size} train step"
-                    if args.model == "unet" else
-                    f"cfg3 STFLSTMUNet(T={args.time_steps}{',PK' if args.pk else ''}) "
-                    f"{args.size}x{args.size} train step")
+        workload = workload_name(args)
         roof = roofline(kt, workload, args.batch, census)
         if gstep is not None and roof:
             roof["timing"] = "dominant kernel timed in one eager step after the timed graph replays"
@@ -295,7 +332,7 @@ def main():
             "metric": "training samples/sec (256x256 DCE-MRI frames)",
             "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
             "execution": "hip_graph" if gstep is not None else "eager",
             "config": {"workload": workload,

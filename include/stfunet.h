@@ -432,6 +432,15 @@ int stf_augment_masks(const uint8_t* src, const stf_aug_frame* masks, int n, con
 const char* stf_error_string(int code);
 int stf_abi_version(void);
 
+/* 16-bit activation storage this library was built for: every entry point above
+ * reads and writes its 16-bit tensors (activations, packed weights, gradients w.r.t.
+ * activations) in this type.  libstfunet_hip.so = bf16, libstfunet_hip_f16.so = fp16
+ * (the reference's autocast(float16) + GradScaler path, train_and_eval.py:389,
+ * train.py:240); same entry points, layouts and constraints otherwise. */
+#define STF_STORAGE_BF16 0
+#define STF_STORAGE_FP16 1
+int stf_storage_type(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,4 +1,4 @@
-"""bf16-storage emulation of the UNet oracle (test infrastructure).
+"""bf16-storage (or fp16-storage) emulation of the UNet oracle (test infrastructure).
 
 Same functional forward as ``oracle.unet`` (src/unet.py:39-57), but every tensor
 the gfx950 path stores in bf16 is rounded to bf16 at the same place, in the
@@ -11,21 +11,37 @@ bf16 storage moves them by ~40 %.  So "kernel correct" is tested as: the HIP
 path's gradient error against the fp32 oracle stays within the band this
 emulation shows against the same oracle (tests/test_unet_gpu.py).
 """
+import contextlib
+
 import torch
 import torch.nn.functional as F
 
 from . import unet as o_unet
+
+STORE = torch.bfloat16       # the emulated 16-bit storage type (``storage(dtype)`` switches it)
+
+
+@contextlib.contextmanager
+def storage(dtype):
+    """Emulate fp16 storage (the gfx950 path's fp16 library) instead of bf16 inside the
+    block; ``oracle.stf_bf16`` rounds through the same ``q``."""
+    global STORE
+    prev, STORE = STORE, dtype
+    try:
+        yield
+    finally:
+        STORE = prev
 
 
 class _Q(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, round_grad):
         ctx.round_grad = round_grad
-        return x.to(torch.bfloat16).float()
+        return x.to(STORE).float()
 
     @staticmethod
     def backward(ctx, g):
-        return (g.to(torch.bfloat16).float() if ctx.round_grad else g), None
+        return (g.to(STORE).float() if ctx.round_grad else g), None
 
 
 def q(x, round_grad=True):

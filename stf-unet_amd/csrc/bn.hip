@@ -159,7 +159,7 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
         for (int j = 0; j < 8; ++j) {
           v[j] = v[j] * sc[j] + sh[j];
           if (relu) v[j] = fmaxf(v[j], 0.f);
-          v[j] = round_bf(v[j]);
+          v[j] = round_e(v[j]);
           mx[j] = d == 0 ? v[j] : fmaxf(mx[j], v[j]);
         }
         *reinterpret_cast<uint4*>(out + p * ocs + cg * 8) = pack8(v);
@@ -226,7 +226,7 @@ __global__ void bn_bwd_reduce_kernel(const uint16_t* __restrict__ dz, int dzcs, 
         for (int j = 0; j < 8; ++j) {
           float t = v[d][j] * sc[j] + sh[j];
           if (mask_mode == 1) t = fmaxf(t, 0.f);
-          a[d][j] = round_bf(t);
+          a[d][j] = round_e(t);
         }
       }
       float dp[8];
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float t = v[j] * sc[j] + sh[j];
-      const float a = round_bf(relu ? fmaxf(t, 0.f) : t);
+      const float a = round_e(relu ? fmaxf(t, 0.f) : t);
       float m = fmaxf(a, quad_xor1(a));
       m = fmaxf(m, quad_xor2(m));
       float c = a == m ? (float)d : 4.f;                       // first maximum of the window

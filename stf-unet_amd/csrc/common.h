@@ -1,34 +1,70 @@
 // Shared device helpers for the STF-Unet gfx950 kernels.
-// Activations are NHWC bf16 (channel-contiguous, 16-B aligned channel groups);
+// Activations are NHWC 16-bit (channel-contiguous, 16-B aligned channel groups);
 // statistics, master weights and gradients are fp32.
+//
+// Storage type: every source is compiled twice (Makefile): bf16 storage
+// (libstfunet_hip.so, the default) and, with -DSTF_FP16, fp16 storage
+// (libstfunet_hip_f16.so: the reference's autocast(float16) + GradScaler numerics,
+// train_and_eval.py:389, train.py:240).  Both are 16-bit with the same layouts, tiles and
+// MFMA rate; only the element type, its conversions and the MFMA opcode differ.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#ifdef STF_FP16
+typedef _Float16 e16;
+#else
+typedef __bf16 e16;
+#endif
+typedef e16 e16x8 __attribute__((ext_vector_type(8)));
+typedef e16 e16x4 __attribute__((ext_vector_type(4)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 #define STF_DEV __device__ __forceinline__
 
 // ---------------------------------------------------------------- conversions
-STF_DEV float bf2f(bf16 v) { return (float)v; }
-STF_DEV bf16 f2bf(float v) { return (bf16)v; }   // v_cvt_pk_bf16_f32: RNE, NaN-preserving
+STF_DEV float e2f(e16 v) { return (float)v; }
+// v_cvt_pk_bf16_f32 / v_cvt_f16_f32: round to nearest even, NaN-preserving
+STF_DEV e16 f2e(float v) { return (e16)v; }
+
+// D += A . B on one 16x16x32 MFMA of the storage type (fp32 accumulation)
+STF_DEV f32x4 mfma16x16x32(e16x8 a, e16x8 b, f32x4 c) {
+#ifdef STF_FP16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+STF_DEV float lo16(uint32_t w) {
+#ifdef STF_FP16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu));
+#else
+  return __uint_as_float(w << 16);
+#endif
+}
+STF_DEV float hi16(uint32_t w) {
+#ifdef STF_FP16
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16));
+#else
+  return __uint_as_float(w & 0xffff0000u);
+#endif
+}
 
 STF_DEV void unpack8(const uint4& u, float (&f)[8]) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    f[2 * i] = lo16(w[i]);
+    f[2 * i + 1] = hi16(w[i]);
   }
 }
 
 STF_DEV uint32_t pack2(float a, float b) {
-  bf16 x = f2bf(a), y = f2bf(b);
+  e16 x = f2e(a), y = f2e(b);
   return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
 }
 
@@ -36,7 +72,7 @@ STF_DEV uint4 pack8(const float (&f)[8]) {
   return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));
 }
 
-STF_DEV float round_bf(float v) { return bf2f(f2bf(v)); }
+STF_DEV float round_e(float v) { return e2f(f2e(v)); }
 
 // LSTM activations on the hardware transcendental units (v_exp_f32, v_rcp_f32): ~1e-7
 // absolute error, far below the bf16 storage of h.  The forward cell, the backward's

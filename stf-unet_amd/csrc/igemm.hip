@@ -84,7 +84,7 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
         const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
         const float c = gf * cp + gi * gg;
         a.c_out[(size_t)m * Ch + ch] = c;
-        reinterpret_cast<bf16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2bf(go * tanh_f(c));
+        reinterpret_cast<e16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2e(go * tanh_f(c));
         if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
         continue;
       }
@@ -96,7 +96,7 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
         const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
         const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
         const float tc = tanh_f(a.c_out[u]);
-        const float h = bf2f(reinterpret_cast<const bf16*>(a.l_dh)[(size_t)m * a.l_dhcs + ch]);
+        const float h = e2f(reinterpret_cast<const e16*>(a.l_dh)[(size_t)m * a.l_dhcs + ch]);
         const float dc = h * go * (1.f - tc * tc) + (a.l_dcn ? a.l_dcn[u] : 0.f);
         const float cp = a.c_prev ? a.c_prev[u] : 0.f;
         const float d_o = h * tc * go * (1.f - go);
@@ -123,13 +123,13 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
       }
       if (a.accumulate) {
         const uint2 old = *reinterpret_cast<const uint2*>(a.dst + off);
-        v[0] += __uint_as_float(old.x << 16);
-        v[1] += __uint_as_float(old.x & 0xffff0000u);
-        v[2] += __uint_as_float(old.y << 16);
-        v[3] += __uint_as_float(old.y & 0xffff0000u);
+        v[0] += lo16(old.x);
+        v[1] += hi16(old.x);
+        v[2] += lo16(old.y);
+        v[3] += hi16(old.y);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = round_bf(v[r]);
+      for (int r = 0; r < 4; ++r) v[r] = round_e(v[r]);
       *reinterpret_cast<uint2*>(a.dst + off) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
 #pragma unroll
       for (int r = 0; r < 4; ++r) { s1[j][r] += v[r]; s2[j][r] += v[r] * v[r]; }
@@ -234,7 +234,7 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
       float o[8];
       unpack8(*reinterpret_cast<const uint4*>(a.dst + off), o);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = round_bf(f[e] + o[e]);
+      for (int e = 0; e < 8; ++e) f[e] = round_e(f[e] + o[e]);
       u = pack8(f);
     }
     *reinterpret_cast<uint4*>(a.dst + off) = u;
@@ -289,7 +289,7 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
   constexpr int PS = HC + 4;                            // fp32 row stride (16-B aligned, skewed)
   constexpr int CCH = HC / 4, HCH = HC / 8;             // 16-B chunks per c row / h row
   float* cs = reinterpret_cast<float*>(smem);           // [BM][PS] c_prev, then c
-  bf16* hs = reinterpret_cast<bf16*>(smem + BM * PS * 4);   // [BM][HC + 8] h
+  e16* hs = reinterpret_cast<e16*>(smem + BM * PS * 4);   // [BM][HC + 8] h
   constexpr int HS = HC + 8;
   const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
   const int Ch = a.Nout >> 2, ch0 = n0 >> 2;
@@ -328,7 +328,7 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
       const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
       const float c = gf * cs[row * PS + hl] + gi * gg;
       cs[row * PS + hl] = c;
-      hs[row * HS + hl] = f2bf(go * tanh_f(c));
+      hs[row * HS + hl] = f2e(go * tanh_f(c));
       if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
     }
   }
@@ -346,10 +346,10 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
     const int r = e / HCH, q = e - r * HCH, m = m0 + r;
     if (!(m < m_end && q * 8 < hcn)) continue;
     uint16_t* dst = a.h_out + (size_t)m * a.hcs + ch0 + q * 8;
-    const bf16* src = hs + r * HS + q * 8;
+    const e16* src = hs + r * HS + q * 8;
     if (hvec && q * 8 + 8 <= hcn) *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     else
-      for (int k = 0; k < 8 && q * 8 + k < hcn; ++k) reinterpret_cast<bf16*>(dst)[k] = src[k];
+      for (int k = 0; k < 8 && q * 8 + k < hcn; ++k) reinterpret_cast<e16*>(dst)[k] = src[k];
   }
 }
 
@@ -370,7 +370,7 @@ STF_DEV void lstm_bwd_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][B
   float* cts = reinterpret_cast<float*>(smem);           // [BM][PS] c_t
   float* cps = cts + BM * PS;                            // [BM][PS] c_{t-1}
   float* dcs = cps + BM * PS;                            // [BM][PS] dc_next, then dc_prev
-  bf16* dhs = reinterpret_cast<bf16*>(dcs + BM * PS);    // [BM][HS] dh
+  e16* dhs = reinterpret_cast<e16*>(dcs + BM * PS);    // [BM][HS] dh
   const int lane = tid & 63, fr = lane & 15, fk = lane >> 4;
   const int Ch = a.Nout >> 2, ch0 = n0 >> 2;
   const int hcn = min(HC, Ch - ch0);
@@ -421,7 +421,7 @@ STF_DEV void lstm_bwd_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][B
       const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
       const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
       const float tc = tanh_f(cts[row * PS + hl]);
-      const float h = bf2f(dhs[row * HS + hl]);
+      const float h = e2f(dhs[row * HS + hl]);
       const float dc = h * go * (1.f - tc * tc) + dcs[row * PS + hl];
       const float cp = cps[row * PS + hl];
       const float d_o = h * tc * go * (1.f - go);
@@ -554,22 +554,22 @@ __global__ __launch_bounds__(NT, 2) void igemm_kernel(Geo a) {
     if (kt + 1 < KT) load_tiles(kt + 1);
     const char* sa = smem + cur * (LDS_A + LDS_B);
     const char* sb = sa + LDS_A;
-    bf16x8 xf[TM], wf[TN];
+    e16x8 xf[TM], wf[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wm * WTM + i * 16 + fr;
-      xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * 64 + swz(row, fk) * 16);
+      xf[i] = *reinterpret_cast<const e16x8*>(sa + row * 64 + swz(row, fk) * 16);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int row = wn * WTN + j * 16 + fr;
-      wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * 64 + swz(row, fk) * 16);
+      wf[j] = *reinterpret_cast<const e16x8*>(sb + row * 64 + swz(row, fk) * 16);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16x16x32(wf[j], xf[i], acc[i][j]);
     if (kt + 1 < KT) store_tiles(cur ^ 1);
     __syncthreads();
   }
@@ -766,22 +766,22 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dm
     const char* sb = sa + BM * ROWB;
 #pragma unroll
     for (int h = 0; h < BKK / 32; ++h) {
-      bf16x8 xf[TM], wf[TN];
+      e16x8 xf[TM], wf[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WTM + i * 16 + fr;
-        xf[i] = *reinterpret_cast<const bf16x8*>(sa + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
+        xf[i] = *reinterpret_cast<const e16x8*>(sa + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WTN + j * 16 + fr;
-        wf[j] = *reinterpret_cast<const bf16x8*>(sb + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
+        wf[j] = *reinterpret_cast<const e16x8*>(sb + row * ROWB + swzk<BKK>(row, fk + 4 * h) * 16);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32(wf[j], xf[i], acc[i][j]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -867,10 +867,10 @@ __global__ __launch_bounds__(NT) void splitk_reduce_kernel(Geo a, int tpg) {
       float o[8];
       unpack8(*reinterpret_cast<const uint4*>(d), o);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[p][e] = round_bf(f[p][e]) + o[e];
+      for (int e = 0; e < 8; ++e) f[p][e] = round_e(f[p][e]) + o[e];
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[p][e] = round_bf(f[p][e]);
+    for (int e = 0; e < 8; ++e) f[p][e] = round_e(f[p][e]);
     *reinterpret_cast<uint4*>(d) = pack8(f[p]);
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] += f[p][e]; s2[e] += f[p][e] * f[p][e]; }
@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     // LDS latency) and the wait is explicit: lgkmcnt(TM + TN) leaves exactly the tap-t+1
     // reads in flight, and it passes tap t's fragments through as operands so no MFMA
     // can be scheduled above it.  All reads have retired (lgkmcnt(0)) by the last tap.
-    bf16x8 xf[2][TM], wf[2][TN];
+    e16x8 xf[2][TM], wf[2][TN];
     const uint32_t hb32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)hb;
     const uint32_t wrow0 = (uint32_t)((HROWS + fr) * 64 + swzh(fr, fk) * 16);    // weight row j*16+fr of tap 0
     auto rd_tap = [&](int t, int b) {
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[b][j], xf[b][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32(wf[b][j], xf[b][i], acc[i][j]);
     }
     stamp(3);
     if (DIRECT && ccc + 1 == CC) {
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
           float o[8];
           unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)m * a.dcs + nt * BN + c16 * 8), o);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = round_bf(f[e] + o[e]);
+          for (int e = 0; e < 8; ++e) f[e] = round_e(f[e] + o[e]);
           u = pack8(f);
         }
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

@@ -102,7 +102,7 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int d0, int d1, 
                                    uint16_t* __restrict__ out) {
   const int total = (int)pack_total(d0, d1, R, S, mode, cpad);
   for (int o = blockIdx.x * NT + threadIdx.x; o < total; o += gridDim.x * NT)
-    reinterpret_cast<bf16*>(out)[o] = f2bf(pack_src(w, d0, d1, R, S, mode, cpad, o));
+    reinterpret_cast<e16*>(out)[o] = f2e(pack_src(w, d0, d1, R, S, mode, cpad, o));
 }
 
 // every descriptor of the list in one launch: blockIdx.y = descriptor
@@ -110,7 +110,7 @@ __global__ void pack_weights_kernel(const stf_pack_desc* __restrict__ descs) {
   const stf_pack_desc d = descs[blockIdx.y];
   const int total = (int)pack_total(d.d0, d.d1, d.R, d.S, d.mode, d.cpad);
   for (int o = blockIdx.x * NT + threadIdx.x; o < total; o += gridDim.x * NT)
-    reinterpret_cast<bf16*>(d.out)[o] = f2bf(pack_src(d.w, d.d0, d.d1, d.R, d.S, d.mode, d.cpad, o));
+    reinterpret_cast<e16*>(d.out)[o] = f2e(pack_src(d.w, d.d0, d.d1, d.R, d.S, d.mode, d.cpad, o));
 }
 
 // Tiled packing (every descriptor of the list in one launch; blockIdx.y = descriptor).
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __r
       uint16_t* o = out + pack_outer_row(d.mode, b0 + b, tap, d.d1, RS) * d.d0 + a0 + q * 8;
       if (q * 8 + 8 <= na) *reinterpret_cast<uint4*>(o) = pack8(v);
       else
-        for (int j = 0; j < na - q * 8; ++j) reinterpret_cast<bf16*>(o)[j] = f2bf(v[j]);
+        for (int j = 0; j < na - q * 8; ++j) reinterpret_cast<e16*>(o)[j] = f2e(v[j]);
     }
   } else {
     const int bext = d.mode == 0 ? d.cpad : d.d1;              // mode 0 rows are cpad wide (zero pad)
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __r
       uint16_t* o = out + ((long)(a0 + a) * RS + tap) * bext + b0 + q * 8;
       if (q * 8 + 8 <= nb) *reinterpret_cast<uint4*>(o) = pack8(v);
       else
-        for (int j = 0; j < nb - q * 8; ++j) reinterpret_cast<bf16*>(o)[j] = f2bf(v[j]);
+        for (int j = 0; j < nb - q * 8; ++j) reinterpret_cast<e16*>(o)[j] = f2e(v[j]);
     }
   }
 }
@@ -337,3 +337,11 @@ extern "C" const char* stf_error_string(int code) {
 }
 
 extern "C" int stf_abi_version(void) { return 6; }
+
+extern "C" int stf_storage_type(void) {
+#ifdef STF_FP16
+  return STF_STORAGE_FP16;
+#else
+  return STF_STORAGE_BF16;
+#endif
+}

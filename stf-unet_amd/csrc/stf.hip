@@ -164,15 +164,15 @@ __global__ void maxpool3_bwd_kernel(const uint8_t* __restrict__ argmax, const ui
 // wcat_t [2C][4C] (its transpose, for the input gradient), bias[4c+q] = b_ih + b_hh
 __global__ void lstm_pack_kernel(const float* __restrict__ wih, const float* __restrict__ whh,
                                  const float* __restrict__ bih, const float* __restrict__ bhh, int C,
-                                 bf16* __restrict__ wcat, bf16* __restrict__ wcat_t, float* __restrict__ bias) {
+                                 e16* __restrict__ wcat, e16* __restrict__ wcat_t, float* __restrict__ bias) {
   const long total = 8L * C * C;
   for (long o = blockIdx.x * (long)NT + threadIdx.x; o < total; o += (long)gridDim.x * NT) {
     const int row = (int)(o / (2 * C)), col = (int)(o - (long)row * 2 * C);   // row = 4c + q
     const int c = row >> 2, q = row & 3;
     const int src_row = q * C + c;
     const float v = col < C ? wih[(long)src_row * C + col] : whh[(long)src_row * C + col - C];
-    wcat[o] = f2bf(v);
-    wcat_t[(long)col * 4 * C + row] = f2bf(v);
+    wcat[o] = f2e(v);
+    wcat_t[(long)col * 4 * C + row] = f2e(v);
     if (col == 0) bias[row] = (bih ? bih[src_row] : 0.f) + (bhh ? bhh[src_row] : 0.f);
   }
 }
@@ -199,7 +199,7 @@ __global__ void lstm_unpack_grad_kernel(const float* __restrict__ dwcat, const f
 //   dg = dc*i*(1-g^2);  df = dc*c_prev*f(1-f);  dc_prev = dc*f
 __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const float* __restrict__ cst,
                                      const float* __restrict__ cprev, const uint16_t* __restrict__ dh, int dhcs,
-                                     const float* dc_in, float* dc_out, bf16* __restrict__ dgates, long M, int C) {
+                                     const float* dc_in, float* dc_out, e16* __restrict__ dgates, long M, int C) {
   const long total = M * C;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < total; u += (long)gridDim.x * NT) {
     const long m = u / C;
@@ -208,7 +208,7 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
     const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
     const float ct = cst[u];
     const float tc = tanh_f(ct);
-    const float h = bf2f(reinterpret_cast<const bf16*>(dh)[m * dhcs + c]);
+    const float h = e2f(reinterpret_cast<const e16*>(dh)[m * dhcs + c]);
     float dc = h * go * (1.f - tc * tc) + (dc_in ? dc_in[u] : 0.f);
     const float cp = cprev ? cprev[u] : 0.f;
     const float d_o = h * tc * go * (1.f - go);
@@ -242,7 +242,7 @@ __global__ void pk_resize_kernel(const float* __restrict__ x, int B, int Ttot, i
     const float* src = x + ((long)b * Ttot + T + p) * H * W;      // frame channel 0 of PK slot p
     const float v = (1.f - ly) * ((1.f - lx) * src[(long)y0 * W + x0] + lx * src[(long)y0 * W + x1]) +
                     ly * ((1.f - lx) * src[(long)y1 * W + x0] + lx * src[(long)y1 * W + x1]);
-    reinterpret_cast<bf16*>(dst)[pix * dcs + coff + p] = f2bf(v);
+    reinterpret_cast<e16*>(dst)[pix * dcs + coff + p] = f2e(v);
   }
 }
 
@@ -302,7 +302,7 @@ extern "C" int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* 
   // hidden sizes 16, 32, ..., 512 (the reference's are 64..512)
   if (C < 16 || C % 16 || 512 % C) return STF_EINVAL;
   hipLaunchKernelGGL(lstm_pack_kernel, dim3(grid_for(8L * C * C, 4096)), dim3(NT), 0, (hipStream_t)stream, w_ih,
-                     w_hh, b_ih, b_hh, C, (bf16*)wcat, (bf16*)wcat_t, bias);
+                     w_hh, b_ih, b_hh, C, (e16*)wcat, (e16*)wcat_t, bias);
   STF_CHECK_LAUNCH();
   return 0;
 }
@@ -320,7 +320,7 @@ extern "C" int stf_lstm_cell_bwd(const float* gates, const float* c_t, const flo
                                  stf_stream_t stream) {
   if (C % 2) return STF_EINVAL;
   hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(grid_for((long)M * C, 8192)), dim3(NT), 0, (hipStream_t)stream,
-                     gates, c_t, c_prev, (const uint16_t*)dh, dh_cstride, dc_in, dc_out, (bf16*)dgates, (long)M, C);
+                     gates, c_t, c_prev, (const uint16_t*)dh, dh_cstride, dc_in, dc_out, (e16*)dgates, (long)M, C);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(WArgs a) {
     const uint16_t* sb = sa + BKP * SA;
 #pragma unroll
     for (int kk = 0; kk < BKP; kk += 32) {
-      bf16x8 af[TM], bfr[TN];
+      e16x8 af[TM], bfr[TN];
       const int krow = kk + 8 * g + q;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(WArgs a) {
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + krow * SA + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + (krow + 4) * SA + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, s8);
+        af[i] = __builtin_bit_cast(e16x8, s8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -131,13 +131,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad_kernel(WArgs a) {
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + krow * SB + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + (krow + 4) * SB + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, s8);
+        bfr[j] = __builtin_bit_cast(e16x8, s8);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32(af[i], bfr[j], acc[i][j]);
     }
     if (it + 1 < steps) store(cur ^ 1);
     __syncthreads();
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       const int col = i * 16 + p4;
       v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][0] + col));
       v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + arow[k2][1] + col));
-      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      return __builtin_bit_cast(e16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     auto readB = [&](int st) {
       const int k2 = st / 9, t = st % 9;
@@ -273,9 +273,9 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       const int col = wn * 16 + p4;
       v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][0] + toff + col));
       v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + brow[k2][1] + toff + col));
-      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      return __builtin_bit_cast(e16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    bf16x8 af[2][TMW], bq[18];
+    e16x8 af[2][TMW], bq[18];
 #pragma unroll
     for (int i = 0; i < TMW; ++i) af[0][i] = readA(0, i);
     bq[0] = readB(0);
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       const int k2 = st / 9, t = st % 9;
 #pragma unroll
       for (int i = 0; i < TMW; ++i)
-        acc[t][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[k2][i], bq[st], acc[t][i][0], 0, 0, 0);
+        acc[t][i][0] = mfma16x16x32(af[k2][i], bq[st], acc[t][i][0]);
       __builtin_amdgcn_sched_barrier(0);        // keep the prefetch distance (no re-clustering)
     }
     if (it + 1 < steps) store(cur ^ 1);
@@ -415,13 +415,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_dma_kernel(WArgs a, int tiles_
     auto rd = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(st + off)); };
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      bf16x8 af[TMW];
+      e16x8 af[TMW];
 #pragma unroll
       for (int i = 0; i < TMW; ++i) {
         v4s lo = rd(aoff[i] + (32 * k2) * 128);
         v4s hi = rd(aoff[i] + (32 * k2 + 8) * 128);
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, s8);
+        af[i] = __builtin_bit_cast(e16x8, s8);
       }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -430,10 +430,10 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_dma_kernel(WArgs a, int tiles_
         v4s lo = rd(boff[0][dx] + imm);
         v4s hi = rd(boff[1][dx] + imm);
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, s8);
+        const e16x8 bfr = __builtin_bit_cast(e16x8, s8);
 #pragma unroll
         for (int i = 0; i < TMW; ++i)
-          acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i], 0, 0, 0);
+          acc[t][i] = mfma16x16x32(af[i], bfr, acc[t][i]);
       }
     }
   }
@@ -540,14 +540,14 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
     const uint16_t* sb = smem + A_EL;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      bf16x8 af[TMW];
+      e16x8 af[TMW];
 #pragma unroll
       for (int i = 0; i < TMW; ++i) {
         const int col = i * 16 + p4;
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][0] + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][1] + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, s8);
+        af[i] = __builtin_bit_cast(e16x8, s8);
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -556,10 +556,10 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + toff + prow[k2][0] + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sb + toff + prow[k2][1] + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, s8);
+        const e16x8 bfr = __builtin_bit_cast(e16x8, s8);
 #pragma unroll
         for (int i = 0; i < TMW; ++i)
-          acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[t][i], 0, 0, 0);
+          acc[t][i] = mfma16x16x32(af[i], bfr, acc[t][i]);
       }
     }
     if (it + 1 < steps) {

@@ -1,19 +1,27 @@
-"""ctypes binding of the gfx950 C-ABI library (include/stfunet.h).
+"""ctypes binding of the gfx950 C-ABI libraries (include/stfunet.h).
 
-The library is built in-tree by ``make -C stf-unet_amd/csrc`` (or
-``__graft_entry__.build()``) into ``stfunet/libstfunet_hip.so``.  There is no
-fallback: if the library is missing or fails to load, every op raises.
-``torch`` is imported first so the HIP runtime torch ships (soname
-``libamdhip64.so.7``) is the one our library binds to -- one runtime per process.
+The sources are built in-tree by ``make -C stf-unet_amd/csrc`` (or
+``__graft_entry__.build()``) twice: ``stfunet/libstfunet_hip.so`` (bf16 activation
+storage, the default) and ``stfunet/libstfunet_hip_f16.so`` (fp16 storage: the
+reference's ``autocast(float16)`` + GradScaler numerics).  Same entry points; the
+launches go to the library of the *active storage dtype* (``storage(dtype)``, set by
+the models around their forward / backward).  There is no fallback: if a library is
+missing or fails to load, every op raises.  ``torch`` is imported first so the HIP
+runtime torch ships (soname ``libamdhip64.so.7``) is the one the libraries bind to --
+one runtime per process.
 """
+import contextlib
 import ctypes
 import os
 
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libstfunet_hip.so")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstfunet_hip.so")
 # A/B measurements: STF_LIB points at another build of the same library (tools/ab_lib.sh)
 LIB_PATH = os.environ.get("STF_LIB", LIB_PATH)
+LIB_PATHS = {torch.bfloat16: LIB_PATH, torch.float16: os.path.join(_HERE, "libstfunet_hip_f16.so")}
+STORAGE_CODE = {torch.bfloat16: 0, torch.float16: 1}     # stf_storage_type()
 
 c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
                                                 ctypes.c_size_t, ctypes.c_int64)
@@ -102,27 +110,71 @@ _SIGS = {
     "stf_pk_resize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "stf_error_string": (ctypes.c_char_p, [c_int]),
     "stf_abi_version": (c_int, []),
+    "stf_storage_type": (c_int, []),
 }
 
 EXPORTED = tuple(_SIGS)
-_lib = None
+_libs = {}
+_active = torch.bfloat16          # storage dtype of the launches issued now
+_FNS = {}                         # dtype -> {entry point name -> bound function}
+_FN = _FNS.setdefault(_active, {})
 
 
-def load():
-    """Load (once) and return the CDLL; raises RuntimeError if unavailable."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"stfunet HIP library not built ({LIB_PATH}); run `make -C stf-unet_amd/csrc` "
+def load(dtype=None):
+    """Load (once) and return the CDLL of ``dtype``'s storage (default: the active
+    one); raises RuntimeError if unavailable or built for another storage type."""
+    dtype = _active if dtype is None else dtype
+    lib = _libs.get(dtype)
+    if lib is not None:
+        return lib
+    if dtype not in LIB_PATHS:
+        raise ValueError(f"no stfunet library for storage dtype {dtype} (bf16 or fp16)")
+    path = LIB_PATHS[dtype]
+    if not os.path.exists(path):
+        raise RuntimeError(f"stfunet HIP library not built ({path}); run `make -C stf-unet_amd/csrc` "
                            "or __graft_entry__.build()")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    if lib.stf_storage_type() != STORAGE_CODE[dtype]:
+        raise RuntimeError(f"{path} was built for another storage type ({lib.stf_storage_type()})")
+    _libs[dtype] = lib
     return lib
+
+
+def storage_dtype():
+    """The 16-bit activation storage dtype the launches issued now use."""
+    return _active
+
+
+def storage_for(requested=None):
+    """The storage a model runs with: ``requested`` (a model's ``storage_dtype``) if set,
+    else fp16 inside ``torch.autocast('cuda', dtype=torch.float16)`` -- the reference's
+    ``--amp`` path (train_and_eval.py:389, autocast's cuda default dtype) -- else bf16."""
+    if requested is not None:
+        return requested
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16:
+        return torch.float16
+    return torch.bfloat16
+
+
+@contextlib.contextmanager
+def storage(dtype):
+    """Route launches to the bf16 or the fp16 library inside the block.  The models
+    enter it around their forward and backward (one model's forward and backward
+    never overlap in time; two models of different storage must not run
+    concurrently)."""
+    global _active, _FN
+    if dtype not in LIB_PATHS:
+        raise ValueError(f"activation storage must be torch.bfloat16 or torch.float16, not {dtype}")
+    prev = _active
+    _active, _FN = dtype, _FNS.setdefault(dtype, {})
+    try:
+        yield
+    finally:
+        _active, _FN = prev, _FNS.setdefault(prev, {})
 
 
 class HipError(RuntimeError):
@@ -141,7 +193,7 @@ _FN = {}
 def call(name, *args):
     f = _FN.get(name)
     if f is None:
-        f = _FN[name] = getattr(load(), name)
+        f = _FN[name] = getattr(load(_active), name)
     rc = f(*args)
     if rc != 0:
         check(rc, name)

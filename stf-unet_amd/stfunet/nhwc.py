@@ -1,7 +1,8 @@
-"""NHWC bf16 feature maps and thin wrappers over the C-ABI kernels.
+"""NHWC 16-bit feature maps and thin wrappers over the C-ABI kernels.
 
-A ``Feat`` is a channel slice of an NHWC bf16 buffer: (buffer, N, H, W, C,
-channel stride, channel offset).  Concat buffers are ordinary buffers whose
+A ``Feat`` is a channel slice of an NHWC 16-bit buffer (bf16, or fp16 when the fp16
+library is active: ``_lib.storage``): (buffer, N, H, W, C, channel stride, channel
+offset).  Concat buffers are ordinary buffers whose
 slices are written by different producers (virtual concat, no copy).
 
 Every wrapper validates shapes on the host before launching (a kernel that
@@ -18,6 +19,11 @@ from . import _lib
 from ._lib import BnrEpi, ConvGeom, IgemmArgs, WgradArgs, call, stream
 
 BF16 = torch.bfloat16
+
+
+def sdt():
+    """16-bit storage dtype of the active library (bf16 or fp16)."""
+    return _lib.storage_dtype()
 
 
 def _p(t):
@@ -115,7 +121,7 @@ def _kernel_name(fn, key, args):
 
 @dataclass
 class Feat:
-    buf: torch.Tensor      # bf16 storage, >= N*H*W*cs elements
+    buf: torch.Tensor      # 16-bit storage (bf16 / fp16), >= N*H*W*cs elements
     N: int
     H: int
     W: int
@@ -135,7 +141,7 @@ class Feat:
         return Feat(self.buf, self.N, self.H, self.W, c, self.cs, self.off + c0)
 
     def check(self):
-        assert self.buf.dtype == BF16 and self.buf.is_cuda
+        assert self.buf.dtype == sdt() and self.buf.is_cuda
         assert self.buf.numel() >= self.M * self.cs, "feature buffer too small"
         assert self.off + self.C <= self.cs
 
@@ -147,12 +153,12 @@ class Feat:
 
 def new_feat(N, H, W, C, device, cs=None):
     cs = cs or C
-    return Feat(torch.empty(N * H * W * cs, dtype=BF16, device=device), N, H, W, C, cs, 0)
+    return Feat(torch.empty(N * H * W * cs, dtype=sdt(), device=device), N, H, W, C, cs, 0)
 
 
 def zeros_feat(N, H, W, C, device, cs=None):
     cs = cs or C
-    return Feat(torch.zeros(N * H * W * cs, dtype=BF16, device=device), N, H, W, C, cs, 0)
+    return Feat(torch.zeros(N * H * W * cs, dtype=sdt(), device=device), N, H, W, C, cs, 0)
 
 
 # ------------------------------------------------------------------ packs
@@ -186,8 +192,13 @@ class PackCache:
         self.recorded = ()
         self.fresh = set()
         self._desc = None
+        self.dtype = None
 
     def refresh(self):
+        if self.dtype != sdt():           # storage type switched: repack everything on demand
+            self.__init__()
+            self.dtype = sdt()
+            return
         if self.seen:
             self.recorded = tuple(self.seen)
         self.seen = {}
@@ -237,14 +248,14 @@ def _pack_into(w, mode, cpad, out, launch=True):
     d0, d1, R, S = w.shape
     n = d0 * R * S * cpad if mode == 0 else d0 * d1 * R * S
     if out is None:
-        out = torch.empty(n, dtype=BF16, device=w.device)
+        out = torch.empty(n, dtype=sdt(), device=w.device)
     if launch:
         call("stf_pack_weight", _p(w), d0, d1, R, S, mode, cpad, _p(out), stream())
     return out
 
 
 def pack_weight(w, mode, cpad=0):
-    """fp32 master weight -> bf16 GEMM rows (modes: include/stfunet.h); served
+    """fp32 master weight -> 16-bit GEMM rows (modes: include/stfunet.h); served
     from the active program's PackCache when one is running."""
     if ACTIVE_PACKS is not None:
         return ACTIVE_PACKS.get(w, mode, cpad)
@@ -252,7 +263,7 @@ def pack_weight(w, mode, cpad=0):
     assert w.dtype == torch.float32 and w.is_contiguous()
     d0, d1, R, S = w.shape
     n = d0 * R * S * cpad if mode == 0 else d0 * d1 * R * S
-    out = torch.empty(n, dtype=BF16, device=w.device)
+    out = torch.empty(n, dtype=sdt(), device=w.device)
     call("stf_pack_weight", _p(w), d0, d1, R, S, mode, cpad, _p(out), stream())
     return out
 
@@ -273,7 +284,7 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
     assert dst.N == src.N and src.N % groups == 0
     if lstm is None:
         assert dst.C == (nout // 4 if scatter2x2 else nout)
-    assert wgt.dtype == BF16 and wgt.numel() == nout * R * S * src.C
+    assert wgt.dtype == sdt() and wgt.numel() == nout * R * S * src.C
     if transposed:
         assert stride in (1, 2)
     else:

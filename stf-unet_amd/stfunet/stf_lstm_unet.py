@@ -186,7 +186,7 @@ class LSTMProgram:
         C, dev = self.C, lbuf.buf.device
         L = self.lstm
         npix = B * lbuf.H * lbuf.W
-        wcat = torch.empty(8 * C * C, dtype=torch.bfloat16, device=dev)
+        wcat = torch.empty(8 * C * C, dtype=nhwc.sdt(), device=dev)
         wcat_t = torch.empty_like(wcat)
         bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
         call("stf_lstm_pack", _p(L.weight_ih_l0.detach()), _p(L.weight_hh_l0.detach()), _p(L.bias_ih_l0.detach()),
@@ -516,9 +516,11 @@ class STFProgram:
 
 class _STFFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, prog, *params):
-        need_bwd = any(ctx.needs_input_grad[2:])
-        logits, saved = prog.forward(x, prog.m.training, need_bwd)
+    def forward(ctx, x, prog, storage, *params):
+        need_bwd = any(ctx.needs_input_grad[3:])
+        with _lib.storage(storage):
+            logits, saved = prog.forward(x, prog.m.training, need_bwd)
+        ctx.storage = storage
         ctx.prog, ctx.saved = prog, saved
         return logits
 
@@ -527,11 +529,12 @@ class _STFFunction(torch.autograd.Function):
         prog = ctx.prog
         dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
-        prog.backward(ctx.saved, dlogits)
+        with _lib.storage(ctx.storage):
+            prog.backward(ctx.saved, dlogits)
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0)
-        return (None, None, *prog.flat.grad_views())
+        return (None, None, None, *prog.flat.grad_views())
 
 
 class STFLSTMUNet(nn.Module):
@@ -565,6 +568,9 @@ class STFLSTMUNet(nn.Module):
         self.final_res = ResidualConvBlock(32, 32)
         self.final = nn.Conv2d(32, num_classes, kernel_size=1)
         self._program = None
+        # 16-bit activation storage: None = bf16, or fp16 under autocast(float16) (the
+        # reference's --amp); torch.bfloat16 / torch.float16 force one (_lib.storage_for)
+        self.storage_dtype = None
 
     @property
     def program(self):
@@ -579,4 +585,4 @@ class STFLSTMUNet(nn.Module):
                                "input to a ROCm device (no CPU fallback)")
         prog = self.program
         prog.flat.ensure()
-        return {"out": _STFFunction.apply(x, prog, *prog.flat.params)}
+        return {"out": _STFFunction.apply(x, prog, _lib.storage_for(self.storage_dtype), *prog.flat.params)}

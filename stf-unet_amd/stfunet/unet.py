@@ -24,7 +24,7 @@ parameter to ``_UNetFunction``, an explicit schedule over NHWC bf16 buffers:
 import torch
 import torch.nn as nn
 
-from . import nhwc
+from . import _lib, nhwc
 from .flat import FlatParams
 from .nhwc import Feat, new_feat
 
@@ -254,9 +254,11 @@ class UNetProgram:
 
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, prog, *params):
-        need_bwd = any(ctx.needs_input_grad[2:])
-        logits, saved = prog.forward(x, prog.m.training, need_bwd)
+    def forward(ctx, x, prog, storage, *params):
+        need_bwd = any(ctx.needs_input_grad[3:])
+        with _lib.storage(storage):
+            logits, saved = prog.forward(x, prog.m.training, need_bwd)
+        ctx.storage = storage
         ctx.prog = prog
         ctx.saved = saved
         return logits
@@ -266,11 +268,12 @@ class _UNetFunction(torch.autograd.Function):
         prog = ctx.prog
         dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
-        prog.backward(ctx.saved, dlogits)
+        with _lib.storage(ctx.storage):
+            prog.backward(ctx.saved, dlogits)
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0)
-        return (None, None, *prog.flat.grad_views())
+        return (None, None, None, *prog.flat.grad_views())
 
 
 class UNet(nn.Module):
@@ -295,6 +298,9 @@ class UNet(nn.Module):
         self.dec1 = _double_conv(base_c * 2, base_c)
         self.out_conv = nn.Conv2d(base_c, num_classes, kernel_size=1)
         self._program = None
+        # 16-bit activation storage: None = bf16, or fp16 under autocast(float16) (the
+        # reference's --amp); torch.bfloat16 / torch.float16 force one (_lib.storage_for)
+        self.storage_dtype = None
 
     @property
     def program(self):
@@ -308,4 +314,4 @@ class UNet(nn.Module):
                                "to a ROCm device (no CPU fallback)")
         prog = self.program
         prog.flat.ensure()
-        return {"out": _UNetFunction.apply(x, prog, *prog.flat.params)}
+        return {"out": _UNetFunction.apply(x, prog, _lib.storage_for(self.storage_dtype), *prog.flat.params)}

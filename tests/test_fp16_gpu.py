@@ -1,0 +1,210 @@
+"""fp16 activation storage (libstfunet_hip_f16.so): the reference's ``--amp`` numerics
+(``autocast(device_type='cuda')`` = float16 + GradScaler, train_and_eval.py:389,
+train.py:240).
+
+Kernel level: the same entry points as the bf16 library, operands rounded to fp16,
+torch fp32 reference; fp16 keeps 3 more mantissa bits than bf16, so the tolerances are
+~8x tighter (relative L2 <= 2e-3 for 16-bit outputs, <= 1e-3 for fp32 outputs).
+
+Model level, against the fp32 oracle (pinned to the reference by tests/golden):
+  logits   relative L2 <= 1.5 x the fp16-storage emulation's own error + 2e-3
+           (oracle.unet_bf16 / oracle.stf_bf16 rounding to fp16 at the same places)
+  loss     |d| <= 2 x the emulation's |d| + 1e-4 (measured: UNet 7e-6, STF 1.5e-4 at the
+           golden input), and the STF loss against the golden value the reference
+           produced (tests/golden/stf_t4.npz) within the same bound
+  Dice     DiceCoefficient (train_and_eval.py:73-142) of the argmax prediction within
+           2 x the emulation's Dice error + 1e-3 of the oracle's at fixed weights.  At
+           initialisation the logits sit near 0 and a few argmax flips move Dice by ~1e-3
+           (measured: STF 2.3e-3 at the golden input), so the north star's "Dice within
+           1e-4" is a property of confident (trained) predictions, not of this point.
+Gradients are not compared element-wise at the whole-model level: at initialisation
+this net's gradients move by 2 % (STF) when the INPUT moves by 1e-6 (fp32 oracle, see
+DESIGN.md "Parity"), so component tests carry the gradient parity.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+F16 = torch.float16
+
+
+def rel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def hr(t):
+    return t.to(F16).float()
+
+
+def feat16(x):
+    from stfunet.nhwc import Feat
+    N, C, H, W = x.shape
+    buf = x.permute(0, 2, 3, 1).contiguous().to(F16).to(DEV)
+    return Feat(buf.view(-1), N, H, W, C, C, 0)
+
+
+@pytest.fixture(autouse=True)
+def _f16():
+    from stfunet import _lib
+    torch.manual_seed(0)
+    with _lib.storage(F16):
+        assert _lib.load().stf_storage_type() == 1
+        yield
+
+
+@pytest.mark.parametrize("cin,cout,H,W,stride,R", [(64, 64, 32, 40, 1, 3), (128, 64, 16, 16, 1, 3),
+                                                    (64, 128, 16, 18, 2, 3), (256, 512, 8, 8, 1, 3),
+                                                    (64, 256, 16, 16, 1, 1)])
+def test_conv_fwd_dgrad_wgrad_fp16(cin, cout, H, W, stride, R):
+    """Forward (+ BN statistics), input gradient and weight gradient on fp16 operands:
+    halo kernel (3x3/s1, W >= 32), linear kernels, strided gather, 1x1."""
+    from stfunet import nhwc
+    pad = R // 2
+    x = hr(torch.randn(2, cin, H, W, device=DEV))
+    w = hr(torch.randn(cout, cin, R, R, device=DEV) / (cin * R * R) ** 0.5)
+    b = torch.randn(cout, device=DEV)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, b, stride=stride, padding=pad)
+    Ho, Wo = ref.shape[2:]
+    dst = nhwc.new_feat(2, Ho, Wo, cout, DEV)
+    assert dst.buf.dtype == F16
+    stats, tiles = nhwc.igemm(feat16(x), nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst, R, R, stride, pad,
+                              bias=b, want_stats=True)
+    out = dst.dense()
+    assert rel(out, ref) < 2e-3
+    s = stats.view(tiles, 2, cout).sum(0)
+    assert rel(s[0], out.sum((0, 2, 3))) < 1e-3
+    dy = hr(torch.randn_like(ref))
+    ref.backward(dy)
+    dx = nhwc.new_feat(2, H, W, cin, DEV)
+    nhwc.conv_dgrad(feat16(dy), w.contiguous(), dx, R, R, stride, pad)
+    assert rel(dx.dense(), xr.grad) < 2e-3
+    dw = torch.empty(cout * cin * R * R, device=DEV)
+    nhwc.wgrad(feat16(dy), feat16(x), R, R, stride, pad, dw)
+    assert rel(dw.view_as(w), wr.grad) < 1e-3
+
+
+def test_lstm_fp16():
+    from stfunet import nhwc
+    from stfunet.stf_lstm_unet import LSTMProgram
+
+    class _G:
+        def __init__(self, m):
+            self.g = {id(p): torch.zeros_like(p) for p in m.parameters()}
+
+        def __call__(self, p):
+            return self.g[id(p)]
+    C, T, B, H = 64, 3, 2, 4
+    lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.copy_(hr(p))
+    npix = B * H * H
+    xs = hr(torch.randn(T, npix, C, device=DEV))
+    lbuf = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+    lbuf.buf.view(T, npix, 2 * C)[:, :, :C] = xs.to(F16)
+    hT = nhwc.new_feat(B, H, H, C, DEV)
+    prog = LSTMProgram(lstm)
+    st = prog.forward(lbuf, T, B, hT)
+    xr = xs.permute(1, 0, 2).contiguous().requires_grad_(True)
+    out, _ = lstm(xr)
+    assert rel(hT.buf.view(npix, C).float(), out[:, -1].detach()) < 3e-3
+    dh = hr(torch.randn(npix, C, device=DEV))
+    out[:, -1].backward(dh)
+    dhf = nhwc.new_feat(B, H, H, C, DEV)
+    dhf.buf.view(npix, C).copy_(dh.to(F16))
+    gv = _G(lstm)
+    dx = prog.backward(st, dhf, gv)
+    assert rel(dx.buf.view(T, npix, 2 * C)[:, :, :C].float(), xr.grad.permute(1, 0, 2)) < 5e-3
+    for name, p in lstm.named_parameters():
+        assert rel(gv(p), p.grad) < 5e-3, name
+
+
+def _oracle(fwd, sd, x, t):
+    from oracle import loss as o_loss
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    p = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        out = fwd(p, x)["out"]
+    return out, o_loss.criterion(out, t).item()
+
+
+def _dice(logits, target):
+    """DiceCoefficient of one batch (train_and_eval.py:80-118, 134-138): mean over classes
+    of the per-class Dice of the argmax prediction (oracle restatement)."""
+    from oracle import metrics as o_metrics
+    return float(o_metrics.dice_per_class(logits.float().cpu(), target.cpu(), logits.shape[1]).mean())
+
+
+@pytest.mark.parametrize("model", ["unet", "stf"])
+def test_model_fp16_vs_oracle(model):
+    """Whole model on the fp16 library (forced storage) vs the fp32 oracle: logits within
+    the fp16 emulation band, loss and Dice at fixed weights."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_stf16, unet as o_unet, unet_bf16 as o_unet16
+    from oracle.cases import dce_case
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet, UNet
+    from stfunet.loss import criterion
+    if model == "unet":
+        m = UNet(in_channels=8, num_classes=2, base_c=16)
+        x5, t = dce_case(1, 2, 8, 64, 64)
+        x = x5.flatten(1, 2)
+        f32 = lambda p, x: o_unet.forward(p, x, training=True)       # noqa: E731
+        emu = lambda p, x: o_unet16.forward(p, x, training=True)     # noqa: E731
+    else:
+        g = np.load(os.path.join(GOLDEN, "stf_t4.npz"))
+        m = STFLSTMUNet(time_steps=4)
+        x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["target"])
+        f32 = lambda p, x: o_stf.forward(p, x, True)                 # noqa: E731
+        emu = lambda p, x: o_stf16.forward(p, x, True)               # noqa: E731
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    m.storage_dtype = F16
+    from stfunet import _lib
+    with _lib.storage(torch.bfloat16):                 # the model itself must switch to fp16
+        out = m(x.to(DEV))["out"].detach()
+        loss = criterion({"out": out}, t.to(DEV)).item()
+    assert m.program.packs.dtype == F16
+    ref, ref_loss = _oracle(f32, sd, x, t)
+    with o_q.storage(F16):
+        emu_out, emu_loss = _oracle(emu, sd, x, t)
+    e_emu = rel(emu_out, ref)
+    assert rel(out, ref) <= 1.5 * e_emu + 2e-3, (rel(out, ref), e_emu)
+    tol = 2 * abs(emu_loss - ref_loss) + 1e-4
+    assert abs(loss - ref_loss) <= tol, (loss, ref_loss, emu_loss)
+    if model == "stf":
+        assert abs(loss - float(g["loss"])) <= tol, (loss, float(g["loss"]))
+    d_ref = _dice(ref, t)
+    assert abs(_dice(out, t) - d_ref) <= 2 * abs(_dice(emu_out, t) - d_ref) + 1e-3
+
+
+def test_autocast_gradscaler_runs_fp16_library():
+    """The reference's --amp step (autocast float16 + GradScaler) through
+    engine.train_one_epoch picks the fp16 library by itself and trains."""
+    from stfunet import _lib, engine
+    from stfunet.optim import AdamW
+    from stfunet.synthetic import dce_batch
+    from stfunet.unet import UNet
+    with _lib.storage(torch.bfloat16):
+        model = UNet(in_channels=8, num_classes=2, base_c=16).to(DEV).train()
+        opt = AdamW([p for p in model.parameters()], lr=1e-3, weight_decay=1e-4)
+        scaler = torch.amp.GradScaler("cuda")
+        batches = [dce_batch(2, 8, 64, 64, seed=s, device=DEV) for s in range(3)]
+        loader = batches                           # train_one_epoch runs preprocess_input itself
+        sched = engine.create_lr_scheduler(opt, len(loader), 1, warmup=True)
+        loss, lr = engine.train_one_epoch(model, opt, loader, torch.device(DEV), 0, 2, lr_scheduler=sched,
+                                          print_freq=100, scaler=scaler)
+        assert np.isfinite(loss) and lr > 0
+        assert model.program.packs.dtype == F16
+        assert all(torch.isfinite(p).all() for p in model.parameters())

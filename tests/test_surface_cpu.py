@@ -39,16 +39,31 @@ def _header_symbols():
     return sorted(set(re.findall(r"\b(stf_[a-z0-9_]+)\s*\(", src)))
 
 
-def test_library_exports_every_header_symbol():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_library_exports_every_header_symbol(dtype):
+    """Both builds (bf16 and fp16 activation storage) export every declared entry point."""
     from stfunet import _lib
-    lib = _lib.load()
+    lib = _lib.load(dtype)
     syms = _header_symbols()
     assert len(syms) >= 20
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
     assert set(syms) == set(_lib.EXPORTED)
     assert lib.stf_abi_version() == 6
+    assert lib.stf_storage_type() == _lib.STORAGE_CODE[dtype]
     assert b"invalid argument" in lib.stf_error_string(100001)
+
+
+def test_storage_selection():
+    from stfunet import _lib
+    assert _lib.storage_dtype() == torch.bfloat16 and _lib.storage_for(None) == torch.bfloat16
+    assert _lib.storage_for(torch.float16) == torch.float16
+    with _lib.storage(torch.float16):
+        assert _lib.storage_dtype() == torch.float16 and _lib.load().stf_storage_type() == 1
+    assert _lib.storage_dtype() == torch.bfloat16
+    with pytest.raises(ValueError):
+        with _lib.storage(torch.float32):
+            pass
 
 
 def test_library_rejects_bad_shapes_without_launch():

@@ -1,7 +1,9 @@
 """Whole-model parity scan: gfx950 path vs the fp32 oracle and vs its bf16-storage
 emulation, at several input sizes (the golden fixtures pin the oracle to the reference at
 64x64; larger inputs give the BatchNorm groups more samples per statistic).
-    python tools/parity_scan.py [--unet]"""
+    python tools/parity_scan.py [--unet] [--fp16]
+--fp16: the model runs on the fp16 library and the emulation rounds to fp16; the loss is
+scaled by 1024 before the backward (GradScaler-style) and the gradients unscaled."""
 import os
 import sys
 import time
@@ -17,6 +19,10 @@ from stfunet.loss import criterion
 
 torch.set_num_threads(16)
 UN = "--unet" in sys.argv
+F16 = "--fp16" in sys.argv
+SCALE = 1024.0 if F16 else 1.0
+import oracle.unet_bf16 as o_q
+o_q.STORE = torch.float16 if F16 else torch.bfloat16
 
 
 def rel(a, b):
@@ -28,7 +34,10 @@ def oracle(fwd, sd, x, t):
     p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     out = fwd(p, x)["out"]
     loss = o_loss.criterion(out, t)
-    loss.backward()
+    (loss * SCALE).backward()
+    for v in p.values():
+        if v.grad is not None:
+            v.grad.div_(SCALE)
     return p, out.detach(), loss.item()
 
 
@@ -50,9 +59,12 @@ for T, S in sizes:
     sd = canonical_state_dict(m.state_dict(), seed=0)
     m.load_state_dict(sd)
     m = m.cuda().train()
+    m.storage_dtype = torch.float16 if F16 else torch.bfloat16
     out = m(x.cuda())["out"]
     loss = criterion({"out": out}, t.cuda())
-    loss.backward()
+    (loss * SCALE).backward()
+    for q_ in m.parameters():
+        q_.grad.div_(SCALE)
     p32, o32, l32 = oracle(f32, sd, x, t)
     pem, oem, lem = oracle(emu, sd, x, t)
     named = dict(m.named_parameters())
