@@ -194,11 +194,15 @@ class PackCache:
         self._desc = None
         self.dtype = None
 
-    def refresh(self):
-        if self.dtype != sdt():           # storage type switched: repack everything on demand
+    def _match_storage(self):
+        """The packed buffers are in the storage type of the library that wrote them:
+        when the active storage changes, forget them (repacked on demand)."""
+        if self.dtype != sdt():
             self.__init__()
             self.dtype = sdt()
-            return
+
+    def refresh(self):
+        self._match_storage()
         if self.seen:
             self.recorded = tuple(self.seen)
         self.seen = {}
@@ -228,6 +232,7 @@ class PackCache:
         self.fresh = set(self.recorded)
 
     def get(self, w, mode, cpad):
+        self._match_storage()
         w = w.detach()
         key = (w.data_ptr(), tuple(w.shape), mode, cpad)
         self.seen[key] = None
