@@ -7,17 +7,22 @@
 #   4. the PK-map fit bench (tools/bench_pk.py) under rocprofv3, the eval-metric micro-bench
 # Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
 set -e
-tag=${1:-r01}
+tag=${1:-r02}
 root=$GRAFT_REPO_ROOT
 out=$root/gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 600 python3 bench.py > $out/bench_unet256_b64.json 2> $out/bench_unet.err
 timeout -k 10 600 python3 bench.py --model stf > $out/bench_stf256_t8_b16.json 2> $out/bench_stf.err
+timeout -k 10 600 python3 bench.py --config 4 --steps 20 --warmup 5 > $out/bench_cfg4_stf256_t16_b16.json 2> $out/bench_cfg4.err
+timeout -k 10 600 python3 bench.py --config 5 --steps 10 --warmup 3 > $out/bench_cfg5_stf512_t32pk_b4_fp16.json 2> $out/bench_cfg5.err
+timeout -k 10 600 python3 bench.py --dtype fp16 --no-cpu-baseline > $out/bench_unet256_b64_fp16.json 2> $out/bench_unet16.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/unet -o run -- \
   python3 $root/bench.py > $out/unet_rocprof_bench.json 2> $out/unet.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stf -o run -- \
   python3 $root/bench.py --model stf > $out/stf_rocprof_bench.json 2> $out/stf.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/cfg5 -o run -- \
+  python3 $root/bench.py --config 5 --steps 10 --warmup 3 --no-cpu-baseline > $out/cfg5_rocprof_bench.json 2> $out/cfg5.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pk -o run -- \
   python3 $root/tools/bench_pk.py > $out/bench_pk.json 2> $out/pk.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/aug -o run -- \
@@ -37,7 +42,8 @@ python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_stf --batch 16 \
 fi
 cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
 cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
+cp $out/cfg5/run_kernel_stats.csv $out/cfg5_stf512_t32pk_b4_fp16_kernel_stats.csv
 cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
 cp $out/aug/run_kernel_stats.csv $out/aug_b16_kernel_stats.csv
-rm -rf $out/unet $out/stf $out/pk $out/aug $out/pmc_unet $out/pmc_stf
+rm -rf $out/unet $out/stf $out/cfg5 $out/pk $out/aug $out/pmc_unet $out/pmc_stf
 ls $out
