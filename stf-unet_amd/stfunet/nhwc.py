@@ -352,8 +352,39 @@ def rows(f: Feat, n0, n):
     return Feat(f.buf[n0 * f.H * f.W * f.cs:], n, f.H, f.W, f.C, f.cs, f.off)
 
 
-def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
-    """Weight gradient into ``out`` (fp32, [dy.C][x.C][R][S] contiguous view)."""
+WGRAD_STREAM = None   # set by a program: weight gradients run there, off the critical path
+_WSTREAMS = {}
+
+
+def wgrad_side_stream(device):
+    """The stream a program's backward sends its weight gradients to, beside the dgrad /
+    BatchNorm chain that carries the critical path (one per device; STF_WGRAD_SIDE=0:
+    inline, for A/B measurements)."""
+    if os.environ.get("STF_WGRAD_SIDE", "1") == "0":
+        return None
+    key = torch.device(device).index
+    if key not in _WSTREAMS:
+        _WSTREAMS[key] = torch.cuda.Stream(device=device)
+    return _WSTREAMS[key]
+
+
+def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
+    """Weight gradient into ``out`` (fp32, [dy.C][x.C][R][S] contiguous view).  With
+    ``WGRAD_STREAM`` set and ``defer``, the launches go to that stream after the current
+    stream's work so far (dy, x complete); the program joins it before ``out`` is read
+    (``defer=False``: ``out`` is consumed right away on the current stream)."""
+    side = WGRAD_STREAM if defer else None
+    if side is not None:
+        main = torch.cuda.current_stream(dy.buf.device)
+        side.wait_stream(main)
+        dy.buf.record_stream(side)
+        x.buf.record_stream(side)
+        with torch.cuda.stream(side):
+            return _wgrad(dy, x, R, S, stride, pad, out)
+    return _wgrad(dy, x, R, S, stride, pad, out)
+
+
+def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
     dy.check()
     x.check()
     assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == dy.C * x.C * R * S

@@ -219,7 +219,7 @@ class LSTMProgram:
             nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
             nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
         dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
-        nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat)
+        nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat, defer=False)
         dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)
         nhwc.channel_sum(dg, dbcat)
         call("stf_lstm_unpack_grad", _p(dwcat), _p(dbcat), C, _p(gv(L.weight_ih_l0)), _p(gv(L.weight_hh_l0)),
@@ -265,6 +265,8 @@ class STFProgram:
     def _done(self, module):
         nhwc.flush_bn_grads()          # grouped BN dgamma/dbeta before the buckets read them
         if self.grad_ready_hook is not None:
+            if nhwc.WGRAD_STREAM is not None:   # the bucket reads this module's weight gradients
+                torch.cuda.current_stream().wait_stream(nhwc.WGRAD_STREAM)
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
@@ -280,9 +282,14 @@ class STFProgram:
 
     def backward(self, S, dlogits):
         nhwc.ACTIVE_PACKS = self.packs
+        ws = nhwc.wgrad_side_stream(dlogits.device)
+        nhwc.WGRAD_STREAM = ws
         try:
             return self._backward(S, dlogits)
         finally:
+            nhwc.WGRAD_STREAM = None
+            if ws is not None:
+                torch.cuda.current_stream(dlogits.device).wait_stream(ws)
             nhwc.flush_bn_grads()
             nhwc.ACTIVE_PACKS = None
 
@@ -496,7 +503,7 @@ class STFProgram:
             nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, gv(w1))
         else:
             tmp = torch.empty(w1.shape[0] * S.xin.C, dtype=torch.float32, device=dev)
-            nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, tmp)
+            nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, tmp, defer=False)
             gv(w1).copy_(tmp.view(w1.shape[0], S.xin.C)[:, :kreal].view(w1.shape))
 
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
@@ -504,7 +511,7 @@ class STFProgram:
         pkb = S.pkbuf[k]
         C = de.C
         tmp = torch.empty(C * pkb.C, dtype=torch.float32, device=de.buf.device)
-        nhwc.wgrad(de, pkb, 1, 1, 1, 0, tmp)
+        nhwc.wgrad(de, pkb, 1, 1, 1, 0, tmp, defer=False)
         gv(fus.weight).copy_(tmp.view(C, pkb.C, 1, 1)[:, :fus.in_channels])
         nhwc.channel_sum(de, gv(fus.bias))
         dpk = new_feat(pkb.N, pkb.H, pkb.W, pkb.C, de.buf.device)

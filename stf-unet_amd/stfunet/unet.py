@@ -107,7 +107,7 @@ class DoubleConvProgram:
             nhwc.wgrad(dy1, src, 3, 3, 1, 1, out)
         else:   # zero-padded input channels (in_channels % 8 != 0): drop the padded columns
             tmp = torch.empty(self.cout * src.C * 9, dtype=torch.float32, device=out.device)
-            nhwc.wgrad(dy1, src, 3, 3, 1, 1, tmp)
+            nhwc.wgrad(dy1, src, 3, 3, 1, 1, tmp, defer=False)
             out.copy_(tmp.view(self.cout, src.C, 3, 3)[:, :cin])
 
 
@@ -129,6 +129,8 @@ class UNetProgram:
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
+            if nhwc.WGRAD_STREAM is not None:   # the bucket reads this module's weight gradients
+                torch.cuda.current_stream().wait_stream(nhwc.WGRAD_STREAM)
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
@@ -143,6 +145,9 @@ class UNetProgram:
             nhwc.ACTIVE_PACKS = None
 
     def backward(self, S, dlogits):
+        # weight gradients stay on the current stream here: a side stream (as in the STF
+        # program) measured +1 % at cfg2 but makes every concurrent kernel's duration (and
+        # so bench.py's per-kernel roofline) a shared-machine number
         nhwc.ACTIVE_PACKS = self.packs
         try:
             return self._backward(S, dlogits)
