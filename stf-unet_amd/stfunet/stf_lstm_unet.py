@@ -309,15 +309,25 @@ class STFProgram:
         # im2col columns (49 (Cf+P) of them, padded): a per-tap gather would pad every tap
         # to 8 channels (8x the MFMA work at Cf = 1) and its weight gradient re-reads dy
         # once per 64 columns
+        # With PK maps (Cf + P = 4 channels) the im2col columns would be 196 per output
+        # pixel (3.5 GB at cfg5's 512^2 x T=32 x B=4): there the input is packed to 8
+        # channels instead and the 7x7/s2 conv gathers its taps (8-channel tap path).
         h2, w2 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         kreal = (Cf + P) * 49
-        kpad = 64 if kreal <= 64 else (kreal + 31) // 32 * 32
-        xin = new_feat(N, h2, w2, kpad, dev)
-        call("stf_stem_im2col", _p(x), B, Ttot, Cf, H, W, T, P, 7, 2, 3, kpad, xin.ptr(), stream())
-        y0 = new_feat(N, h2, w2, 64, dev)
         w1 = m.conv1.weight
-        stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, kpad), 64, y0, 1, 1, 1, 0,
-                                  want_stats=training, groups=T)
+        y0 = new_feat(N, h2, w2, 64, dev)
+        S.stem_gather = Cf + P > 1 and Cf + P <= 8
+        if S.stem_gather:
+            xin = new_feat(N, H, W, 8, dev)
+            call("stf_pack_sequence", _p(x), B, Ttot, Cf, H, W, T, P, 8, xin.ptr(), stream())
+            stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1, 0, 8), 64, y0, 7, 7, 2, 3,
+                                      want_stats=training, groups=T)
+        else:
+            kpad = 64 if kreal <= 64 else (kreal + 31) // 32 * 32
+            xin = new_feat(N, h2, w2, kpad, dev)
+            call("stf_stem_im2col", _p(x), B, Ttot, Cf, H, W, T, P, 7, 2, 3, kpad, xin.ptr(), stream())
+            stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, kpad), 64, y0, 1, 1,
+                                      1, 0, want_stats=training, groups=T)
         S.bn0 = nhwc.bn_finalize(stats, tiles, m.bn1, y0.M, training, T)
         a0 = new_feat(N, h2, w2, 64, dev)
         nhwc.bn_act(y0, S.bn0, a0)
@@ -499,7 +509,11 @@ class STFProgram:
         dy0 = nhwc.bn_backward(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), dz=da0)
         w1 = m.conv1.weight
         kreal = w1[0].numel()
-        if S.xin.C == kreal:
+        if S.stem_gather:                      # 8-channel packed input, 7x7/s2 gather
+            tmp = torch.empty(w1.shape[0] * 8 * 49, dtype=torch.float32, device=dev)
+            nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp, defer=False)
+            gv(w1).copy_(tmp.view(w1.shape[0], 8, 7, 7)[:, :w1.shape[1]])
+        elif S.xin.C == kreal:
             nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, gv(w1))
         else:
             tmp = torch.empty(w1.shape[0] * S.xin.C, dtype=torch.float32, device=dev)
