@@ -340,6 +340,24 @@ int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W
  * interleaved (src/stf_lstm_unet.py:124-127).  C in {16, 32, ..., 512} (STF_EINVAL otherwise). */
 int stf_lstm_pack(const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh,
                   int C, void* wcat, void* wcat_t, float* bias, stf_stream_t stream);
+/* The whole forward sequence of nn.LSTM(C, C) in one launch (src/stf_lstm_unet.py:214-242):
+ * lbuf = [T][P][2C] 16-bit rows of step t = [x_t | h_{t-1}] (x_t given, the h slots of
+ * steps 1..T-1 are written here, step 0's is ignored: h_{-1} = 0), wcat / bias from
+ * stf_lstm_pack, c_out = [T][P][C] fp32 cell states, h_{T-1} -> h_last (stride h_cstride).
+ * Same values as T launches of stf_igemm with the LSTM cell epilogue.  C = 64 only
+ * (stf_lstm_seq_supported); 16-B aligned wcat / lbuf. */
+int stf_lstm_seq_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
+                     void* h_last, int h_cstride, stf_stream_t stream);
+int stf_lstm_seq_supported(int C);
+/* The whole backward (BPTT) of that sequence in one launch: recomputes every step's gates
+ * from lbuf (as the forward computed them), runs the cell backward and the input-gradient
+ * GEMM; dgates = [T][P][4C] 16-bit pre-activation gate gradients (for the weight gradient
+ * afterwards), dx = rows [T][P] of stride dx_cstride receiving dL/dx_t in channels [0, C);
+ * dh_last = dL/dh_{T-1} (stride dh_cstride).  Same values as the per-step path (stf_igemm
+ * with the LSTM backward epilogue + the dgates x W GEMM).  C = 64 only; 16-B alignment. */
+int stf_lstm_seq_bwd(const void* wcat, const void* wcat_t, const float* bias, const void* lbuf, int P, int T,
+                     int C, const float* c_all, const void* dh_last, int dh_cstride, void* dgates, void* dx,
+                     int dx_cstride, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
 int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,
                          float* dw_hh, float* db_ih, float* db_hh, stf_stream_t stream);

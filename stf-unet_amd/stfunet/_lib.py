@@ -106,6 +106,9 @@ _SIGS = {
     "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "stf_lstm_pack": (c_int, [P, P, P, P, c_int, P, P, P, P]),
     "stf_lstm_unpack_grad": (c_int, [P, P, c_int, P, P, P, P, P]),
+    "stf_lstm_seq_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P]),
+    "stf_lstm_seq_supported": (c_int, [c_int]),
+    "stf_lstm_seq_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P]),
     "stf_lstm_cell_bwd": (c_int, [P, P, P, P, c_int, P, P, P, c_int64, c_int, P]),
     "stf_pk_resize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
     "stf_error_string": (ctypes.c_char_p, [c_int]),

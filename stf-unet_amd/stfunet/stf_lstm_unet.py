@@ -24,6 +24,8 @@ Schedule (all NHWC bf16, fp32 statistics; ``STFProgram``):
   * backward mirrors it (BPTT = per-step cell kernel + one GEMM; LSTM weight
     gradients = one GEMM over all T steps).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -182,6 +184,12 @@ class LSTMProgram:
         self.lstm = lstm
         self.C = lstm.hidden_size
 
+    def fused(self, lbuf: Feat, hT: Feat):
+        """Whole-sequence kernel (stf_lstm_seq_fwd) for this hidden size and layout?
+        STF_LSTM_SEQ=0 keeps the per-step launches (A/B)."""
+        return (os.environ.get("STF_LSTM_SEQ", "1") != "0" and bool(_lib.load().stf_lstm_seq_supported(self.C))
+                and lbuf.off == 0 and lbuf.cs == 2 * self.C and hT.cs >= self.C)
+
     def forward(self, lbuf: Feat, T, B, hT: Feat):
         C, dev = self.C, lbuf.buf.device
         L = self.lstm
@@ -192,13 +200,21 @@ class LSTMProgram:
         call("stf_lstm_pack", _p(L.weight_ih_l0.detach()), _p(L.weight_hh_l0.detach()), _p(L.bias_ih_l0.detach()),
              _p(L.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias), stream())
         cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
-        for t in range(T):
-            src = rows(lbuf, t * B, B)
-            hdst = rows(lbuf, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
-            epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, None)
-            nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
+        fused = self.fused(lbuf, hT)
+        if fused:
+            # all T steps in one launch: c in registers, h_{t-1} in LDS (same values)
+            lbuf.check()
+            hT.check()
+            call("stf_lstm_seq_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs, stream())
+        else:
+            for t in range(T):
+                src = rows(lbuf, t * B, B)
+                hdst = rows(lbuf, (t + 1) * B, B).slice(C, C) if t < T - 1 else hT
+                epi = LstmEpi(_p(cst[t - 1]) if t > 0 else None, _p(cst[t]), hdst.ptr(), hdst.cs, None)
+                nhwc.igemm(src, wcat, 4 * C, src, 1, 1, 1, 0, bias=bias, lstm=epi)
         st = _S()
         st.lbuf, st.T, st.B, st.wcat, st.wcat_t, st.bias, st.c = lbuf, T, B, wcat, wcat_t, bias, cst
+        st.fused = fused
         return st
 
     def backward(self, st, dhT: Feat, gv):
@@ -208,16 +224,22 @@ class LSTMProgram:
         npix = B * lb.H * lb.W
         d2 = new_feat(T * B, lb.H, lb.W, 2 * C, dev)           # rows of step t: [dx_t | dh_{t-1}]
         dg = new_feat(T * B, lb.H, lb.W, 4 * C, dev)           # pre-activation gate grads (interleaved)
-        dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
-        for t in range(T - 1, -1, -1):
-            dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
-            dgt = rows(dg, t * B, B)
-            src = rows(lb, t * B, B)
-            # recompute step t's gates (same GEMM as the forward) + cell backward epilogue
-            epi = LstmEpi(_p(st.c[t - 1]) if t > 0 else None, _p(st.c[t]), None, 0, None,
-                          1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
-            nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
-            nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
+        if st.fused:
+            # all T steps backward in one launch (dc in registers, dh_{t-1} in LDS)
+            dhT.check()
+            call("stf_lstm_seq_bwd", _p(st.wcat), _p(st.wcat_t), _p(st.bias), lb.ptr(), npix, T, C, _p(st.c),
+                 dhT.ptr(), dhT.cs, dg.ptr(), d2.ptr(), d2.cs, stream())
+        else:
+            dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
+            for t in range(T - 1, -1, -1):
+                dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
+                dgt = rows(dg, t * B, B)
+                src = rows(lb, t * B, B)
+                # recompute step t's gates (same GEMM as the forward) + cell backward epilogue
+                epi = LstmEpi(_p(st.c[t - 1]) if t > 0 else None, _p(st.c[t]), None, 0, None,
+                              1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
+                nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
+                nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
         dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
         nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat, defer=False)
         dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)

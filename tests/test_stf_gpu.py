@@ -311,3 +311,30 @@ def test_stf_eval_mode_vs_oracle():
     assert rel(out, ref) <= 2 * e_emu + 2e-3, (rel(out, ref), e_emu)
     for k, v in m.state_dict().items():                     # eval never moves the statistics
         assert torch.equal(v.cpu(), sd[k]), k
+
+
+@pytest.mark.parametrize("T,B,H", [(5, 3, 6), (1, 2, 8), (8, 16, 8)])
+def test_lstm_whole_sequence_equals_per_step(monkeypatch, T, B, H):
+    """stf_lstm_seq_fwd / _bwd (C = 64: all T steps in one launch, 64 pixels per
+    workgroup, ragged last workgroup when B*H*H % 64 != 0) produce bit for bit the
+    per-step launches' h_T, cell states, [x | h] rows, input and weight gradients."""
+    from stfunet import nhwc
+    from stfunet.stf_lstm_unet import LSTMProgram
+    C = 64
+    lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
+    lbuf = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+    lbuf.buf.view(-1, 2 * C)[:, :C].normal_()
+    dhT = nhwc.new_feat(B, H, H, 3 * C, DEV).slice(C, C)       # strided h_T gradient (decoder slice)
+    dhT.buf.normal_()
+    prog = LSTMProgram(lstm)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("STF_LSTM_SEQ", mode)
+        hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
+        st = prog.forward(lbuf, T, B, hT)
+        assert st.fused == (mode == "1")
+        gv = _Grads(lstm)
+        dx = prog.backward(st, dhT, gv)
+        out[mode] = [hT.dense(), st.c, lbuf.buf.clone(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b)
