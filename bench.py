@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timer", action="store_true")
+    ap.add_argument("--no-dice", action="store_true", help="skip the trained-weight Dice-vs-reference leg")
     a = ap.parse_args()
     presets = {2: dict(model="unet", batch=64, size=256, time_steps=8, pk=False, dtype="bf16"),
                3: dict(model="stf", batch=16, size=256, time_steps=8, pk=False, dtype="bf16"),
@@ -140,6 +141,40 @@ def doubleconv_report(blocks):
                      "block_tflops": round(bt, 1), "block_mfma_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 3),
                      "conv_ms": round(cms, 3), "block_ms": round(bms, 3)}
     return out
+
+
+def dice_vs_reference(dev, dtype):
+    """BASELINE metric's "Dice vs ref": the reference-trained UNet(in=8, base_c=8) of
+    tests/golden/unet_trained.npz (make_golden_trained.py: trained by the reference's own
+    train_one_epoch, parameters rounded to bf16, Dice from its own evaluate()) evaluated by
+    engine.evaluate on this build's gfx950 path on the same 4 held-out batches (seeded
+    splitmix DCE stacks, regenerated by stfunet.synthetic -- no oracle code).  The fixture
+    is data (inputs' seeds, weights, the reference's Dice), not a CPU path."""
+    import numpy as np
+    from stfunet import UNet, engine
+    from stfunet.synthetic import splitmix_dce_case
+    z = np.load(os.path.join(HERE, "tests", "golden", "unet_trained.npz"))
+    base_c, b, t, hw, _, _, n_eval = (int(v) for v in z["config"])
+    model = UNet(in_channels=8, num_classes=2, base_c=base_c)
+    sd = model.state_dict()
+    for k, v in sd.items():
+        if "bf16." + k in z.files:
+            bits = z["bf16." + k].astype(np.uint32) << 16
+            sd[k] = torch.from_numpy(bits.view(np.float32).reshape(v.shape).copy())
+        else:
+            sd[k] = torch.from_numpy(z["state." + k].copy()).reshape(v.shape)
+    model.load_state_dict(sd)
+    model.storage_dtype = torch.float16 if dtype == "fp16" else torch.bfloat16
+    model = model.to(dev)
+    data = [splitmix_dce_case(2000 + i, b, t, hw, hw) for i in range(n_eval)]
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):          # evaluate()'s MetricLogger lines stay off stdout
+        got = engine.evaluate(model, data, dev, num_classes=2)
+    ref = float(z["dice"])
+    return {"value": round(got["dice"], 7), "reference": round(ref, 7), "abs_diff": abs(got["dice"] - ref),
+            "tolerance": 1e-4, "storage": dtype,
+            "sample": f"reference-trained UNet(in=8, base_c={base_c}), eval mode, {n_eval} held-out batches "
+                      f"[{b}, {t}, 1, {hw}, {hw}] (tests/golden/unet_trained.npz)"}
 
 
 def cpu_baseline(args):
@@ -349,6 +384,8 @@ def main():
                                     for k, d in census.items()},
             "last_loss": round(last_loss, 5),
         }
+        if not args.no_dice:
+            res["dice_vs_ref"] = dice_vs_reference(dev, args.dtype)
         if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)

@@ -40,3 +40,40 @@ def dce_batch(batch, time_steps, height, width, seed=0, device="cuda", pk_channe
     if mask_hw is not None:
         target = target[:, :: height // mask_hw[0], :: width // mask_hw[1]].contiguous()
     return img.contiguous(), target
+
+
+_SM1, _SM2, _SM3 = 0x9E3779B97F4A7C15, 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+
+
+def _splitmix_uniform(seed, stream, n):
+    """n float64 values in [-1, 1) from the counter-based splitmix64 stream (seed, stream, i): the
+    generator the parity fixtures were written with (platform-independent, bit-reproducible)."""
+    import numpy as np
+    m = np.uint64(0xFFFFFFFFFFFFFFFF)
+    base = np.uint64((seed * 0x100000001B3 + stream * 0x9E3779B1) & 0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        z = (np.arange(n, dtype=np.uint64) + (base << np.uint64(20))) + np.uint64(_SM1)
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(_SM2)) & m
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(_SM3)) & m
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
+
+
+def splitmix_dce_case(seed, batch, time_steps, height, width):
+    """Deterministic CPU DCE stack + disc mask of the fixture set (tests/golden/make_golden*.py):
+    background 0.5 + U(-0.3, 0.3), two discs per image whose intensity rises by 0.25 t/T, normalised
+    like train.py:147-148.  Returns (image [B, T, 1, H, W] fp32, mask [B, H, W] int64)."""
+    import numpy as np
+    b, t, h, w = batch, time_steps, height, width
+    img = _splitmix_uniform(seed, 0, b * t * h * w).reshape(b, t, 1, h, w) * 0.3 + 0.5
+    geo = (_splitmix_uniform(seed, 1, b * 8).reshape(b, 8) + 1.0) / 2.0
+    yy, xx = np.mgrid[0:h, 0:w]
+    mask = np.zeros((b, h, w), np.int64)
+    for i in range(b):
+        for d in range(2):
+            cy, cx, r = geo[i, 3 * d] * h, geo[i, 3 * d + 1] * w, 3 + geo[i, 3 * d + 2] * h / 5
+            disc = (yy - cy) ** 2 + (xx - cx) ** 2 <= r * r
+            mask[i][disc] = 1
+            for tt in range(t):
+                img[i, tt, 0][disc] += 0.25 * (tt + 1) / t
+    return torch.from_numpy(((img - 0.709) / 0.127).astype(np.float32)), torch.from_numpy(mask)

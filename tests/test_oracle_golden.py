@@ -182,3 +182,21 @@ def test_pk_tofts_oracle_vs_reference():
     for k in range(3):
         assert ((maps[k] - ref[k]).norm() / ref[k].norm()).item() < 1e-6
         assert (maps[k] - ref[k]).abs().max().item() < 1e-6
+
+
+def test_trained_unet_dice_oracle_vs_reference():
+    """Trained-weight Dice (tests/golden/make_golden_trained.py: the reference trained UNet(base_c=8)
+    with its own train_one_epoch, then its evaluate()): the fp32 oracle's eval-mode forward gives the
+    same argmax on every pixel and the same Dice."""
+    import _trained
+    tr = _trained.load()
+    p = _trained.shaped(tr["state"], o_unet.template_state_dict(8, 2, tr["base_c"]))
+    preds, dices = [], []
+    with torch.no_grad():
+        for x5, t in tr["eval"]:
+            out = o_unet.forward(p, x5.flatten(1, 2), training=False)["out"]
+            preds.append(out.argmax(1).numpy())
+            dices.append(o_metrics.dice_per_class(out, t, 2, ignore_index=255))
+    assert np.array_equal(np.concatenate(preds), tr["pred"])
+    assert abs(float(np.mean(dices, axis=0).mean()) - tr["dice"]) < 1e-6
+    assert tr["dice"] > 0.98

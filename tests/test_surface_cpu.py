@@ -108,3 +108,14 @@ def test_engine_metrics_match_reference():
     dc.update(torch.from_numpy(g["logits_absent"]), torch.from_numpy(g["target_absent"]))
     assert np.allclose(dc.compute().numpy(), g["dice_per_class"], atol=1e-6)
     assert abs(dc.value.item() - float(g["dice_value"])) < 1e-6
+
+
+def test_product_synthetic_cases_match_fixture_generator():
+    """stfunet.synthetic.splitmix_dce_case (bench.py's Dice leg) regenerates the fixture inputs
+    bit for bit (oracle.cases.dce_case wrote them)."""
+    import torch
+    from oracle.cases import dce_case
+    from stfunet.synthetic import splitmix_dce_case
+    for seed in (0, 5, 2003):
+        a, b = dce_case(seed, 2, 8, 32, 48), splitmix_dce_case(seed, 2, 8, 32, 48)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
