@@ -140,6 +140,10 @@ typedef struct stf_wgrad_args {
   const void* x;       /* bf16 source (gathered as in stf_conv_geom)            */
   float* ws;           /* workspace [splits][Nout][R*S*Cs] fp32                 */
   int splits;          /* pixel splits (from stf_wgrad_plan)                    */
+  int grid_blocks;     /* workgroups the pixel split aims at (0: two per CU).   */
+                       /* A weight gradient running on a side stream beside the */
+                       /* dgrad / BatchNorm chain asks for one per CU, so the   */
+                       /* chain's kernels still find registers on every CU (ABI v7) */
 } stf_wgrad_args;
 
 /* Choose splits and report workspace bytes for a weight-gradient pass. */

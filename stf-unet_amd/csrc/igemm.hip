@@ -1430,6 +1430,16 @@ int halo_min_w() {
   static const int v = [] { const char* e = getenv("STF_HALO_MINW"); return e ? atoi(e) : 16; }();
   return v;
 }
+// the halo kernel's persistent grid needs enough (pixel tile, 64-channel slice) items to
+// fill the chip; below STF_HALO_MIN_ITEMS the linear kernels (with split-K) run instead
+int halo_min_items() {
+  static const int v = [] { const char* e = getenv("STF_HALO_MIN_ITEMS"); return e ? atoi(e) : 0; }();
+  return v;
+}
+long halo_items(const stf_conv_geom& c, int nout) {
+  const long ty = (c.Hd + halo_ph() - 1) / halo_ph(), tx = (c.Wd + halo_pw(c) - 1) / halo_pw(c);
+  return (long)c.N * ty * tx * (nout / 64);
+}
 // direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad),
 // =2 always (default: measured 1.7 % faster on the forward convs than the LDS-staged one)
 bool halo_direct(const stf_igemm_args* a) {
@@ -1513,7 +1523,9 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   // auto: the halo kernel for full-size 3x3 layers ('L' = auto over the linear kernels only)
   // (measured, tools/ab_minw.sh: at 16 <= W < 32 the 16x16 halo tile wins up to 256 output
   // channels, the 256x256 linear tile above that)
-  if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= halo_min_w() && a->Nout <= 256))) return 'H';
+  if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= halo_min_w() && a->Nout <= 256)) &&
+      halo_items(c, a->Nout) >= halo_min_items())
+    return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
     if ((plain || a->scatter2x2) && bk64 && !a->lstm && !c.transposed) return f;

@@ -667,7 +667,8 @@ void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
     const long tiles = (long)(a->Nout / 64) * (a->g.Cs / 64);
-    long want = (512 + tiles - 1) / tiles;
+    const long target = a->grid_blocks > 0 ? a->grid_blocks : 512;
+    long want = (target + tiles - 1) / tiles;
     const long maxs = (nt + 3) / 4;                  // at least 4 pixel tiles per split
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;

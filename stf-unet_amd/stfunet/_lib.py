@@ -53,7 +53,7 @@ class IgemmArgs(ctypes.Structure):
 
 class WgradArgs(ctypes.Structure):
     _fields_ = [("g", ConvGeom), ("dy", P), ("dy_cstride", c_int), ("Nout", c_int), ("x", P),
-                ("ws", P), ("splits", c_int)]
+                ("ws", P), ("splits", c_int), ("grid_blocks", c_int)]
 
 
 # name -> (restype, argtypes)

@@ -380,16 +380,29 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
         dy.buf.record_stream(side)
         x.buf.record_stream(side)
         with torch.cuda.stream(side):
-            return _wgrad(dy, x, R, S, stride, pad, out)
+            # one workgroup per CU beside the critical path (two per CU inline): the
+            # fused kernel's two 250-register waves per SIMD would leave the dgrad /
+            # BatchNorm chain no registers on any CU (STF cfg3 11.3-11.5 vs 11.8-12.3 ms)
+            return _wgrad(dy, x, R, S, stride, pad, out, _num_cus(dy.buf.device))
     return _wgrad(dy, x, R, S, stride, pad, out)
 
 
-def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out):
+_CUS = {}
+
+
+def _num_cus(device):
+    n = _CUS.get(device)
+    if n is None:
+        n = _CUS[device] = torch.cuda.get_device_properties(device).multi_processor_count
+    return n
+
+
+def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
     dy.check()
     x.check()
     assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == dy.C * x.C * R * S
     g = ConvGeom(x.N, x.H, x.W, x.C, x.cs, dy.H, dy.W, R, S, stride, pad, 0)
-    a = WgradArgs(g, dy.ptr(), dy.cs, dy.C, x.ptr(), None, 0)
+    a = WgradArgs(g, dy.ptr(), dy.cs, dy.C, x.ptr(), None, 0, grid_blocks)
     splits = ctypes.c_int(0)
     nbytes = ctypes.c_size_t(0)
     call("stf_wgrad_plan", ctypes.byref(a), ctypes.byref(splits), ctypes.byref(nbytes))

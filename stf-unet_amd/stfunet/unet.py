@@ -21,6 +21,8 @@ parameter to ``_UNetFunction``, an explicit schedule over NHWC bf16 buffers:
   OutConv (src/unet.py:37,56): fused with dec1's last BN+ReLU in stf_head_fwd
   backward: the mirror schedule, gradients written into one flat fp32 buffer.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -149,9 +151,14 @@ class UNetProgram:
         # program) measured +1 % at cfg2 but makes every concurrent kernel's duration (and
         # so bench.py's per-kernel roofline) a shared-machine number
         nhwc.ACTIVE_PACKS = self.packs
+        ws = nhwc.wgrad_side_stream(dlogits.device) if os.environ.get("STF_UNET_WGRAD_SIDE") == "1" else None
+        nhwc.WGRAD_STREAM = ws
         try:
             return self._backward(S, dlogits)
         finally:
+            nhwc.WGRAD_STREAM = None
+            if ws is not None:
+                torch.cuda.current_stream(dlogits.device).wait_stream(ws)
             nhwc.ACTIVE_PACKS = None
 
     def _forward(self, x, training, need_bwd):

@@ -1,11 +1,13 @@
 """List every implicit-GEMM / wgrad launch of one STF (or UNet) training step with its
-shape, chosen device kernel and FLOPs, aggregated (launch counts per shape).
+shape, chosen device kernel and FLOPs, aggregated (launch counts per shape).  Weight
+gradients run inline (STF_WGRAD_SIDE=0) so that the events bracket them.
     python tools/stf_shapes.py [--unet]"""
 import os
 import sys
 from collections import defaultdict
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "stf-unet_amd")]
+os.environ["STF_WGRAD_SIDE"] = "0"
 import torch
 from stfunet import nhwc, engine, STFLSTMUNet, UNet
 from stfunet.synthetic import dce_batch
@@ -32,9 +34,9 @@ def igemm(src, wgt, nout, dst, R, S, stride, pad, transposed=False, **kw):
     return r
 
 
-def wgrad(dy, x, R, S, stride, pad, out):
+def wgrad(dy, x, R, S, stride, pad, out, **kw):
     e0 = torch.cuda.Event(enable_timing=True); e0.record()
-    r = orig_wgrad(dy, x, R, S, stride, pad, out)
+    r = orig_wgrad(dy, x, R, S, stride, pad, out, **kw)
     e1 = torch.cuda.Event(enable_timing=True); e1.record()
     key = f"wgrad dy {dy.N}x{dy.H}x{dy.W}x{dy.C} x {x.H}x{x.W}x{x.C} k{R}s{stride}"
     if TIME:
