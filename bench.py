@@ -384,7 +384,7 @@ def main():
                                     for k, d in census.items()},
             "last_loss": round(last_loss, 5),
         }
-        if not args.no_dice:
+        if not args.no_dice and world == 1:    # evaluate() all-reduces: rank 0 alone must not call it at N > 1
             res["dice_vs_ref"] = dice_vs_reference(dev, args.dtype)
         if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args)
