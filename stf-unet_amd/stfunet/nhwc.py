@@ -375,16 +375,44 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
     (``defer=False``: ``out`` is consumed right away on the current stream)."""
     side = WGRAD_STREAM if defer else None
     if side is not None:
-        main = torch.cuda.current_stream(dy.buf.device)
-        side.wait_stream(main)
+        # host fast path (the STF step issues ~55 of these and is host-bound): one pooled
+        # event instead of wait_stream's fresh Event, torch's current stream switched by id
+        main = WGRAD_MAIN
+        if main is None or _lib.stream().value != main.cuda_stream:   # e.g. called on another side stream
+            main = torch.cuda.current_stream()
+        ev = _sync_event()
+        ev.record(main)
+        side.wait_event(ev)
         dy.buf.record_stream(side)
         x.buf.record_stream(side)
-        with torch.cuda.stream(side):
+        _set_stream(side)
+        try:
             # one workgroup per CU beside the critical path (two per CU inline): the
             # fused kernel's two 250-register waves per SIMD would leave the dgrad /
             # BatchNorm chain no registers on any CU (STF cfg3 11.3-11.5 vs 11.8-12.3 ms)
             return _wgrad(dy, x, R, S, stride, pad, out, _num_cus(dy.buf.device))
+        finally:
+            _set_stream(main)
     return _wgrad(dy, x, R, S, stride, pad, out)
+
+
+WGRAD_MAIN = None     # the program's main stream while WGRAD_STREAM is set
+_EVENTS = []
+_EV_NEXT = [0]
+
+
+def _sync_event():
+    """Cross-stream sync events, reused round robin: a stream wait enqueued on an event
+    keeps waiting for the record it saw, so re-recording one later is safe."""
+    if len(_EVENTS) < 64:
+        _EVENTS.append(torch.cuda.Event())
+        return _EVENTS[-1]
+    i = _EV_NEXT[0] = (_EV_NEXT[0] + 1) % len(_EVENTS)
+    return _EVENTS[i]
+
+
+def _set_stream(s):
+    torch._C._cuda_setStream(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
 
 
 _CUS = {}
@@ -393,7 +421,8 @@ _CUS = {}
 def _num_cus(device):
     n = _CUS.get(device)
     if n is None:
-        n = _CUS[device] = torch.cuda.get_device_properties(device).multi_processor_count
+        n = torch.cuda.get_device_properties(device).multi_processor_count
+        n = _CUS[device] = int(os.environ.get("STF_SIDE_WGRAD_BLOCKS", n))    # A/B override
     return n
 
 

@@ -306,10 +306,11 @@ class STFProgram:
         nhwc.ACTIVE_PACKS = self.packs
         ws = nhwc.wgrad_side_stream(dlogits.device)
         nhwc.WGRAD_STREAM = ws
+        nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device)
         try:
             return self._backward(S, dlogits)
         finally:
-            nhwc.WGRAD_STREAM = None
+            nhwc.WGRAD_STREAM = nhwc.WGRAD_MAIN = None
             if ws is not None:
                 torch.cuda.current_stream(dlogits.device).wait_stream(ws)
             nhwc.flush_bn_grads()

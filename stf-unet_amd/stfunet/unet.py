@@ -153,10 +153,11 @@ class UNetProgram:
         nhwc.ACTIVE_PACKS = self.packs
         ws = nhwc.wgrad_side_stream(dlogits.device) if os.environ.get("STF_UNET_WGRAD_SIDE") == "1" else None
         nhwc.WGRAD_STREAM = ws
+        nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device) if ws is not None else None
         try:
             return self._backward(S, dlogits)
         finally:
-            nhwc.WGRAD_STREAM = None
+            nhwc.WGRAD_STREAM = nhwc.WGRAD_MAIN = None
             if ws is not None:
                 torch.cuda.current_stream(dlogits.device).wait_stream(ws)
             nhwc.ACTIVE_PACKS = None

@@ -12,7 +12,5 @@ run() {  # tag "ENV=.. ENV=.." "bench args"
 }
 run eager "STF_AB=0" "--graph off"
 run graph "STF_AB=0" "--graph on"
-# DEBUG_HIP_FORCE_GRAPH_QUEUES=1/4: same as the default (13.0 ms); =8 segfaulted in the runtime
-run graph_nopc "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0" "--graph on"
-run graph_nopc_q4 "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_HIP_FORCE_GRAPH_QUEUES=4" "--graph on"
 run eager2 "STF_AB=0" "--graph off"
+run graph2 "STF_AB=0" "--graph on"

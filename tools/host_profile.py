@@ -43,6 +43,8 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
+# backward on this thread, so that cProfile sees the programs' backward schedule too
+torch.autograd.set_multithreading_enabled(False)
 pr = cProfile.Profile()
 pr.enable()
 for _ in range(a.steps):
@@ -51,3 +53,4 @@ pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(a.top)
+st.sort_stats("cumulative").print_stats(a.top)
