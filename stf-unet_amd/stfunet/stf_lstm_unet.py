@@ -273,6 +273,7 @@ class STFProgram:
         self.lstms = [m.lstm1, m.lstm2, m.lstm3, m.lstm4]
         self.lstm_progs = [LSTMProgram(lstm) for lstm in self.lstms]
         self._side = None
+        self._wstream = None
 
     def side_streams(self, dev):
         """One HIP stream per LSTM scale 1-3.  The four per-pixel LSTMs are independent
@@ -287,8 +288,8 @@ class STFProgram:
     def _done(self, module):
         nhwc.flush_bn_grads()          # grouped BN dgamma/dbeta before the buckets read them
         if self.grad_ready_hook is not None:
-            if nhwc.WGRAD_STREAM is not None:   # the bucket reads this module's weight gradients
-                torch.cuda.current_stream().wait_stream(nhwc.WGRAD_STREAM)
+            if self._wstream is not None:       # the bucket reads this module's weight gradients
+                torch.cuda.current_stream().wait_stream(self._wstream)
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
@@ -304,7 +305,7 @@ class STFProgram:
 
     def backward(self, S, dlogits):
         nhwc.ACTIVE_PACKS = self.packs
-        ws = nhwc.wgrad_side_stream(dlogits.device)
+        ws = self._wstream = nhwc.wgrad_side_stream(dlogits.device)
         nhwc.WGRAD_STREAM = ws
         nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device)
         try:
