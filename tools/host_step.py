@@ -13,6 +13,7 @@ import torch
 ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="unet")
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--time-steps", type=int, default=8)
 a = ap.parse_args()
 from stfunet import engine, STFLSTMUNet, UNet
 from stfunet.optim import AdamW
@@ -23,7 +24,8 @@ torch.manual_seed(0)
 if a.model == "unet":
     model, B, T, half = UNet(in_channels=8, num_classes=2, base_c=64).to(dev), 64, 8, None
 else:
-    model, B, T, half = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8).to(dev), 16, 8, (128, 128)
+    T = a.time_steps
+    model, B, half = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T).to(dev), 16, (128, 128)
 model.train()
 opt = AdamW(model.parameters(), lr=1e-3)
 x, t = dce_batch(B, T, 256, 256, seed=1, device=dev, mask_hw=half)
