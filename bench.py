@@ -101,6 +101,25 @@ def pmc_traffic(kernel, workload, batch):
     return None, None
 
 
+def pmc_mfma(kernel, workload):
+    """MFMA busy fraction of ``kernel`` from the committed PMC pass of the same workload
+    (tools/pmc_mfma.sh + tools/pmc_mfma_summary.py: SQ_VALU_MFMA_BUSY_CYCLES over
+    GRBM_GUI_ACTIVE/8 x 1024 SIMDs, i.e. at the clock the chip held); None when absent."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(HERE, "profiles", "r*", "pmc_mfma*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != workload:
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        return ({"mfma_busy_util": k["mfma_busy_util"], "clock_ghz": k["clock_ghz"], "source": os.path.relpath(path, HERE)}
+                if k else None)
+    return None
+
+
 def roofline(kt, workload, batch, census):
     """Roofline of the dominant kernel (largest summed time in the census step;
     its every launch in the timed region bracketed by HIP events on its launch
@@ -116,7 +135,8 @@ def roofline(kt, workload, batch, census):
     return {"bound": "mfma", "kernel": name, "achieved": round(k["tflops"], 2), "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC 2*FETCH_SIZE+WRITE_SIZE)",
-            "traffic_source": src, "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
+            "traffic_source": src, "pmc_mfma": pmc_mfma(name, workload),
+            "launches": k["launches"], "avg_launch_us": round(k["avg_us"], 2),
             "algorithmic_tflop_per_launch": round(k["flops"] / k["launches"] / 1e12, 6),
             "all_conv_gemm_kernels_census_step": {
                 "ms": round(gemm_ms, 3), "tflops": round(gemm_fl / (gemm_ms * 1e-3) / 1e12, 2) if gemm_ms else 0.0}}

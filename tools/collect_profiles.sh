@@ -33,6 +33,14 @@ timeout -k 10 200 python3 tools/bench_aug.py > $out/bench_aug.json 2> $out/bench
 if [ -z "$SKIP_PMC" ]; then
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_unet --steps 3 --warmup 1
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_stf --model stf --steps 3 --warmup 1
+bash tools/pmc_mfma.sh gpurun_out/prof_$tag/mfma_unet --steps 3 --warmup 1
+bash tools/pmc_mfma.sh gpurun_out/prof_$tag/mfma_stf --model stf --steps 3 --warmup 1
+python3 tools/pmc_mfma_summary.py gpurun_out/prof_$tag/mfma_unet --unet-layers \
+  --workload "cfg2 UNet(in=8,base_c=64) 256x256 train step" --command "bash tools/pmc_mfma.sh OUT --steps 3 --warmup 1" \
+  --json $out/pmc_mfma_unet256_b64.json > $out/pmc_mfma_unet256_b64_summary.txt
+python3 tools/pmc_mfma_summary.py gpurun_out/prof_$tag/mfma_stf \
+  --workload "cfg3 STFLSTMUNet(T=8) 256x256 train step" --command "bash tools/pmc_mfma.sh OUT --model stf --steps 3 --warmup 1" \
+  --json $out/pmc_mfma_stf256_t8_b16.json > $out/pmc_mfma_stf256_t8_b16_summary.txt
 python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_unet --batch 64 \
   --workload "cfg2 UNet(in=8,base_c=64) 256x256 train step" \
   --command "bash tools/pmc_passes.sh OUT --steps 3 --warmup 1" --json $out/pmc_traffic_unet256_b64.json > $out/pmc_unet256_b64_summary.txt
@@ -45,5 +53,5 @@ cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
 cp $out/cfg5/run_kernel_stats.csv $out/cfg5_stf512_t32pk_b4_fp16_kernel_stats.csv
 cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
 cp $out/aug/run_kernel_stats.csv $out/aug_b16_kernel_stats.csv
-rm -rf $out/unet $out/stf $out/cfg5 $out/pk $out/aug $out/pmc_unet $out/pmc_stf
+rm -rf $out/unet $out/stf $out/cfg5 $out/pk $out/aug $out/pmc_unet $out/pmc_stf $out/mfma_unet $out/mfma_stf
 ls $out
