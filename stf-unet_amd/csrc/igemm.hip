@@ -40,6 +40,9 @@ struct Geo {
   // split-K (plain DMA kernels): blockIdx.z = K slice, fp32 partials [ksplit][M][Nout] in ws,
   // folded by splitk_reduce_kernel (bias, bf16 store, BN statistics)
   int ksplit; float* ws;
+  // halo kernel: keep a ring stage's weight rows across items when they are the rows
+  // the next fill needs (same 64-channel output slice and source chunk)
+  int wkeep;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -958,7 +961,12 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 
   // live = false: a dummy stage (all lanes out of range) so every iteration issues the same DMA count
   // DMA instructions k0 .. k1-1 of this wave's HI halo + WI weight instructions
-  auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1) {
+  // weight rows held by each ring stage: key nt * CC + cc (wave-uniform, every wave tracks
+  // the same sequence).  With an even chunk count a stage holds the same source chunk for
+  // every item, so within one output slice its weight rows never change and the refill
+  // of the stage only streams the halo (half the DMA instructions at 64 source channels).
+  int wkey0 = -1, wkey1 = -1;
+  auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1, bool wload) {
     const int nt = item / ntiles, tile = item - nt * ntiles;
     const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
@@ -977,7 +985,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     }
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
-      if (HI + i < k0 || HI + i >= k1) continue;
+      if (HI + i < k0 || HI + i >= k1 || !wload) continue;
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
@@ -990,7 +998,18 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
           0, 0);
     }
   };
-  auto issue = [&](int item, int cc, int buf, bool live) { issue_part(item, cc, buf, live, 0, HI + WI); };
+  auto issue = [&](int item, int cc, int buf, bool live, bool wload = true) {
+    issue_part(item, cc, buf, live, 0, HI + WI, wload);
+  };
+  // does filling stage buf with (item, cc) need the weight DMA?  (and record what it holds)
+  auto need_w = [&](int item, int cc, int buf, bool live) {
+    if (STAGES != 2 || !a.wkeep || !live) return true;
+    const int key = (item / ntiles) * CC + cc;
+    int& held = buf ? wkey1 : wkey0;
+    const bool need = held != key;
+    held = key;
+    return need;
+  };
 
   // byte offset (within a stage) of this lane's halo read for fragment i at tap column dx,
   // tap row 0: the swizzle is keyed on the halo column, so the tap row dy only adds the
@@ -1011,7 +1030,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (STAGES == 2) issue(it0, 0, 0, true);
+  if (STAGES == 2) issue(it0, 0, 0, true, need_w(it0, 0, 0, true));
   int iit = it0, icc = 0;                               // issue cursor (last issued stage)
   int cit = it0, ccc = 0;                               // compute cursor
   // BN partial statistics, one row per (group, workgroup): stats [groups][gridDim][2][Nout].
@@ -1033,6 +1052,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
         sbuf[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = 0.f;
   }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
+  bool wl_next = true;                                   // the next fill streams weight rows too
   // DIAG 4: per-wave cycle buckets (s_memtime) -- DMA wait, barrier, DMA issue, taps, epilogue
   uint64_t tb[5] = {0, 0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
@@ -1072,11 +1092,12 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       load_bias();
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
+      wl_next = need_w(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
       // even waves issue the next stage's DMA now, odd waves after tap 4: the address
       // path takes ~300 cycles per 1-KiB LDS-DMA instruction under load, and with all
       // eight waves issuing at once both waves of a SIMD stalled together (DIAG 4: a third
       // of the time); staggered, one wave of each SIMD computes while the other issues
-      if (!STAGGER || !(wave & 1)) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
+      if (!STAGGER || !(wave & 1)) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1), wl_next);
       stamp(2);
     } else {
       // single stage: every wave is done with the buffer, refill it, wait
@@ -1114,7 +1135,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     for (int t = 0; t < 9; ++t) {
       const int b = t & 1;
       if constexpr (STAGGER) {
-        if (t == 4 && (wave & 1)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1));
+        if (t == 4 && (wave & 1)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
       }
       if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
       // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
@@ -1194,6 +1215,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
         aff_pre[2] = a.bnr_mean[o]; aff_pre[3] = a.bnr_invstd[o];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
+        (buf ? wkey1 : wkey0) = -1;                     // the y rows overwrite its weight rows
         const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
             (void*)a.bnr_y, 0, (uint32_t)((size_t)a.M * a.bnr_ycs * 2), 0x00020000);
 #pragma unroll
@@ -1325,6 +1347,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       char* ot = smem + buf * STAGE;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                     // every wave is done reading this stage
+      (buf ? wkey1 : wkey0) = -1;                       // the output tile overwrites its weight rows
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int p = wave * WTM + i * 16 + fr;
@@ -1762,6 +1785,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.bnr_relu = 0; g.bnr_part = nullptr;
   g.par = 0;
   g.ksplit = 1; g.ws = nullptr;
+  static const int wkeep = [] { const char* e = getenv("STF_HALO_WKEEP"); return e ? atoi(e) : 1; }();
+  g.wkeep = wkeep;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
