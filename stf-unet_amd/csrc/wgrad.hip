@@ -23,6 +23,7 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 struct WArgs {
   const uint16_t* dy; const uint16_t* x; float* ws;
   int N, Hs, Ws, Cs, xcs, Hd, Wd, R, S, st, pad, M, Nout, dycs, chunk;
+  int colmajor;         // fused 3x3: walk pixel tiles column-major (vertical neighbours in turn)
 };
 
 template <int BM, int BN, int BKP, bool GENERAL>
@@ -193,7 +194,11 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   uint4 ra[CHA], rb[CHB];
   auto load = [&](int t) {
     const int img = t / per_img, rem = t - img * per_img;
-    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    // column-major: the next tile is the one below, whose halo shares two of the (PH + 2)
+    // rows just fetched (L2 hits) -- row-major neighbours share only two columns
+    int ty, tx;
+    if (a.colmajor) { tx = rem / tiles_y; ty = rem - tx * tiles_y; }
+    else { ty = rem / tiles_x; tx = rem - ty * tiles_x; }
     const int y0 = ty * PH, x0 = tx * PW;
 #pragma unroll
     for (int i = 0; i < CHA; ++i) {
@@ -723,6 +728,8 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.N = c.N; w.Hs = c.Hs; w.Ws = c.Ws; w.Cs = c.Cs; w.xcs = c.src_cstride; w.Hd = c.Hd; w.Wd = c.Wd;
   w.R = c.R; w.S = c.S; w.st = c.stride; w.pad = c.pad; w.M = c.N * c.Hd * c.Wd; w.Nout = a->Nout;
   w.dycs = a->dy_cstride; w.chunk = chunk;
+  static const int colmajor = [] { const char* e = getenv("STF_WGRAD_COLMAJOR"); return e ? atoi(e) : 1; }();
+  w.colmajor = colmajor;
   hipStream_t s = (hipStream_t)stream;
   const int rsc = c.R * c.S * c.Cs;
   if (const int pw = fused_pw(a)) {
