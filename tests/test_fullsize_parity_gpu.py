@@ -1,0 +1,167 @@
+"""Parity at BASELINE.json's full sizes against the fp32 restatement run on the GPU.
+
+The oracle (oracle/unet.py, oracle/stf.py) is plain functional torch, so here it runs on
+the GPU in fp32 (torch's own convolutions) at configs[1] (UNet(in=8, base_c=64), 256^2,
+B=64) and configs[2] (STFLSTMUNet T=8, 256^2, B=16) -- the same checks as the small-size
+tests, at the benchmarked shapes.  The bf16-storage emulation (oracle/*_bf16.py, fp32 math
+with every stored activation rounded to bf16) runs beside it to set the rounding band:
+
+  UNet train mode   logits rel-L2 <= 3e-2, |loss| <= 1e-2, running stats <= 2e-2,
+                    parameter gradients err_hip <= 2 * err_emu + 0.03 (as tests/test_unet_gpu.py)
+  UNet eval mode    logits rel-L2 <= 2 * err_emu + 2e-3; argmax (the prediction evaluate()
+                    scores with Dice) flipped vs fp32 on at most 2 * flips_emu + 1e-4 of the
+                    4.2 M pixels, and |Dice_hip - Dice_fp32| <= 2 * |Dice_emu - Dice_fp32| + 1e-4
+  STF eval mode     logits rel-L2 <= 2 * err_emu + 2e-3 (as test_stf_eval_mode_vs_oracle)
+"""
+import pytest
+import torch
+
+from oracle import loss as o_loss, unet as o_unet, unet_bf16 as o_unet_bf16
+from oracle.init import canonical_state_dict
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _fp32_reference():
+    """The reference runs in true fp32 (no reduced-precision matmul paths) on torch's native
+    im2col + rocBLAS convolutions: MIOpen would compile kernels for every new shape on a
+    fresh box (~1 min per batch size), the native path starts at once (0.4 s per step)."""
+    old = torch.backends.cudnn.enabled, torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cudnn.enabled = False
+    torch.backends.cuda.matmul.allow_tf32 = False
+    yield
+    torch.backends.cudnn.enabled, torch.backends.cuda.matmul.allow_tf32 = old
+
+
+def rel(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _bn_fed_bias(k):
+    return k.endswith((".0.bias", ".3.bias")) and not k.startswith(("up", "out_conv"))
+
+
+def _unet(seed=0):
+    from stfunet import UNet
+    m = UNet(in_channels=8, num_classes=2, base_c=64)
+    sd = canonical_state_dict(m.state_dict(), seed=seed)
+    m.load_state_dict(sd)
+    return m.to(DEV), {k: v.to(DEV) for k, v in sd.items()}
+
+
+def _oracle_train(sd, x, t, fwd):
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    out = fwd(p, x, training=True)["out"]
+    loss = o_loss.criterion(out, t)
+    loss.backward()
+    return p, out.detach(), loss.item()
+
+
+def _dice(logits, t):
+    """Foreground Dice of the argmax prediction (train_and_eval.py:316-374 scoring)."""
+    pred = logits.argmax(1)
+    inter = ((pred == 1) & (t == 1)).sum().double()
+    return (2 * inter / ((pred == 1).sum() + (t == 1).sum()).double().clamp_min(1)).item(), pred
+
+
+def test_unet_cfg2_fullsize_train_vs_fp32():
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    model, sd = _unet()
+    x, t = dce_batch(64, 8, 256, 256, seed=5, device=DEV)
+    x = x.flatten(1, 2)
+    p, ref_out, ref_loss = _oracle_train(sd, x, t, o_unet.forward)
+    pe, _, _ = _oracle_train(sd, x, t, o_unet_bf16.forward)
+    model.train()
+    out = model(x)["out"]
+    loss = criterion({"out": out}, t)
+    loss.backward()
+    assert rel(out, ref_out) < 3e-2, rel(out, ref_out)
+    assert abs(loss.item() - ref_loss) < 1e-2, (loss.item(), ref_loss)
+    named = dict(model.named_parameters())
+    bad, worst = [], (0.0, 0.0, "")
+    for k, v in p.items():
+        if v.grad is None:
+            continue
+        got = named[k].grad
+        if _bn_fed_bias(k):     # exact gradient 0 (a BatchNorm follows): absolute check
+            scale = v.grad.abs().max().item() + p[k.replace("bias", "weight")].grad.abs().mean().item()
+            if got.abs().max().item() > 0.05 * scale + 1e-5:
+                bad.append((k, "bias", got.abs().max().item()))
+            continue
+        e_hip, e_emu = rel(got, v.grad), rel(pe[k].grad, v.grad)
+        if e_hip > 2 * e_emu + 0.03:
+            bad.append((k, e_hip, e_emu))
+        worst = max(worst, (e_hip - 2 * e_emu, e_hip, k))
+    print(f"\nUNet cfg2 train: logits rel {rel(out, ref_out):.3e}, loss {loss.item():.6f} vs {ref_loss:.6f}, "
+          f"tightest gradient {worst[2]} rel {worst[1]:.3e} (band 2*emu+0.03)")
+    assert not bad, bad
+    msd = model.state_dict()
+    for k in sd:
+        if "running" in k:
+            assert rel(msd[k], p[k]) < 2e-2, k
+
+
+def test_unet_cfg2_fullsize_eval_dice_vs_fp32():
+    from stfunet.synthetic import dce_batch
+    model, sd = _unet(seed=1)
+    gen = torch.Generator().manual_seed(7)
+    for k, v in sd.items():     # fixed statistics: eval mode, no BatchNorm amplification
+        if "running_mean" in k:
+            sd[k] = (torch.rand(v.shape, generator=gen) - 0.5).to(DEV)
+        if "running_var" in k:
+            sd[k] = (torch.rand(v.shape, generator=gen) * 1.5 + 0.5).to(DEV)
+    model.load_state_dict(sd)
+    model.eval()
+    x, t = dce_batch(64, 8, 256, 256, seed=6, device=DEV)
+    x = x.flatten(1, 2)
+    with torch.no_grad():
+        out = model(x)["out"].float()
+        ref = o_unet.forward(sd, x, training=False)["out"]
+        emu = o_unet_bf16.forward(sd, x, training=False)["out"]
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    print(f"\nSTF cfg3 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
+    assert e_hip <= 2 * e_emu + 2e-3, (e_hip, e_emu)
+    d_ref, p_ref = _dice(ref, t)
+    d_hip, p_hip = _dice(out, t)
+    d_emu, p_emu = _dice(emu, t)
+    n = p_ref.numel()
+    f_hip = (p_hip != p_ref).sum().item() / n
+    f_emu = (p_emu != p_ref).sum().item() / n
+    print(f"\nUNet cfg2 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e}), argmax flips {f_hip:.2e} (emu {f_emu:.2e}), "
+          f"Dice {d_hip:.6f} vs fp32 {d_ref:.6f} (emu {d_emu:.6f})")
+    assert f_hip <= 2 * f_emu + 1e-4, (f_hip, f_emu)
+    assert abs(d_hip - d_ref) <= 2 * abs(d_emu - d_ref) + 1e-4, (d_hip, d_ref, d_emu)
+    for k, v in model.state_dict().items():                 # eval never moves the statistics
+        assert torch.equal(v, sd[k]), k
+
+
+def test_stf_cfg3_fullsize_eval_vs_fp32():
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    gen = torch.Generator().manual_seed(3)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.2 - 0.1
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.5 + 0.75
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, _ = dce_batch(16, 8, 256, 256, seed=8, device=DEV, mask_hw=(128, 128))
+    with torch.no_grad():
+        out = m(x)["out"].float()
+        ref = o_stf.forward(sd, x, False)["out"]
+        with o_q.storage(torch.bfloat16):
+            emu = o_emu.forward(sd, x, False)["out"]
+    assert out.shape == (16, 2, 128, 128)
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    print(f"\nSTF cfg3 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
+    assert e_hip <= 2 * e_emu + 2e-3, (e_hip, e_emu)
