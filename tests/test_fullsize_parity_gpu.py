@@ -82,7 +82,7 @@ def test_unet_cfg2_fullsize_train_vs_fp32():
     assert rel(out, ref_out) < 3e-2, rel(out, ref_out)
     assert abs(loss.item() - ref_loss) < 1e-2, (loss.item(), ref_loss)
     named = dict(model.named_parameters())
-    bad, worst = [], (0.0, 0.0, "")
+    bad, worst = [], (-1.0, 0.0, 0.0, "")
     for k, v in p.items():
         if v.grad is None:
             continue
@@ -95,9 +95,9 @@ def test_unet_cfg2_fullsize_train_vs_fp32():
         e_hip, e_emu = rel(got, v.grad), rel(pe[k].grad, v.grad)
         if e_hip > 2 * e_emu + 0.03:
             bad.append((k, e_hip, e_emu))
-        worst = max(worst, (e_hip - 2 * e_emu, e_hip, k))
+        worst = max(worst, (e_hip / (2 * e_emu + 0.03), e_hip, e_emu, k))
     print(f"\nUNet cfg2 train: logits rel {rel(out, ref_out):.3e}, loss {loss.item():.6f} vs {ref_loss:.6f}, "
-          f"tightest gradient {worst[2]} rel {worst[1]:.3e} (band 2*emu+0.03)")
+          f"tightest gradient {worst[3]}: rel {worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
     assert not bad, bad
     msd = model.state_dict()
     for k in sd:
@@ -119,11 +119,15 @@ def test_unet_cfg2_fullsize_eval_dice_vs_fp32():
     x, t = dce_batch(64, 8, 256, 256, seed=6, device=DEV)
     x = x.flatten(1, 2)
     with torch.no_grad():
+        # shift the head bias so that the fp32 reference predicts both classes about equally
+        # (at initialisation one class wins everywhere and Dice would compare 0 with 0)
+        ref = o_unet.forward(sd, x, training=False)["out"]
+        sd["out_conv.bias"][1] += (ref[:, 0] - ref[:, 1]).median()
+        model.load_state_dict(sd)
         out = model(x)["out"].float()
         ref = o_unet.forward(sd, x, training=False)["out"]
         emu = o_unet_bf16.forward(sd, x, training=False)["out"]
     e_hip, e_emu = rel(out, ref), rel(emu, ref)
-    print(f"\nSTF cfg3 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
     assert e_hip <= 2 * e_emu + 2e-3, (e_hip, e_emu)
     d_ref, p_ref = _dice(ref, t)
     d_hip, p_hip = _dice(out, t)
@@ -131,7 +135,7 @@ def test_unet_cfg2_fullsize_eval_dice_vs_fp32():
     n = p_ref.numel()
     f_hip = (p_hip != p_ref).sum().item() / n
     f_emu = (p_emu != p_ref).sum().item() / n
-    print(f"\nUNet cfg2 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e}), argmax flips {f_hip:.2e} (emu {f_emu:.2e}), "
+    print(f"\nUNet cfg2 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e}, hip vs emu {rel(out, emu):.3e}), argmax flips {f_hip:.2e} (emu {f_emu:.2e}), "
           f"Dice {d_hip:.6f} vs fp32 {d_ref:.6f} (emu {d_emu:.6f})")
     assert f_hip <= 2 * f_emu + 1e-4, (f_hip, f_emu)
     assert abs(d_hip - d_ref) <= 2 * abs(d_emu - d_ref) + 1e-4, (d_hip, d_ref, d_emu)
@@ -165,3 +169,54 @@ def test_stf_cfg3_fullsize_eval_vs_fp32():
     e_hip, e_emu = rel(out, ref), rel(emu, ref)
     print(f"\nSTF cfg3 eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
     assert e_hip <= 2 * e_emu + 2e-3, (e_hip, e_emu)
+
+
+def test_unet_cfg2_fullsize_eval_fp16_storage_vs_fp32():
+    """The reference's --amp numerics (fp16 activation storage, libstfunet_hip_f16.so)."""
+    from stfunet.synthetic import dce_batch
+    model, sd = _unet(seed=2)
+    model.storage_dtype = torch.float16
+    model.eval()
+    x, _ = dce_batch(64, 8, 256, 256, seed=9, device=DEV)
+    x = x.flatten(1, 2)
+    with torch.no_grad():
+        out = model(x)["out"].float()
+        ref = o_unet.forward(sd, x, training=False)["out"]
+        with o_unet_bf16.storage(torch.float16):
+            emu = o_unet_bf16.forward(sd, x, training=False)["out"]
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    print(f"\nUNet cfg2 eval, fp16 storage: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
+    assert e_hip <= 2 * e_emu + 2e-4, (e_hip, e_emu)
+
+
+@pytest.mark.parametrize("T", [8, 16])
+def test_stf_fullsize_train_vs_fp32(T):
+    """configs[2] (T=8) and configs[3]'s per-GPU workload (T=16), B=16, 256^2, train mode:
+    loss and logits within the bf16-emulation band (whole-model STF gradients are chaotic
+    under 16-bit storage at initialisation -- see tests/test_stf_gpu.py -- so they are only
+    checked finite here; the components carry the gradient parity)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = dce_batch(16, T, 256, 256, seed=10 + T, device=DEV, mask_hw=(128, 128))
+    with torch.no_grad():
+        ref = o_stf.forward({k: v.clone() for k, v in sd.items()}, x, True)["out"]
+        with o_q.storage(torch.bfloat16):
+            emu = o_emu.forward({k: v.clone() for k, v in sd.items()}, x, True)["out"]
+    out = m(x)["out"]
+    loss = criterion({"out": out}, t)
+    loss.backward()
+    ref_loss = o_loss.criterion(ref, t).item()
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    print(f"\nSTF T={T} train: logits rel {e_hip:.3e} (emu {e_emu:.3e}, hip vs emu {rel(out, emu):.3e}), loss {loss.item():.5f} vs {ref_loss:.5f}")
+    assert e_hip <= 2 * e_emu + 0.05, (e_hip, e_emu)
+    assert abs(loss.item() - ref_loss) < 0.03
+    for k, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), k
