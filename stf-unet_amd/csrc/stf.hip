@@ -286,7 +286,7 @@ extern "C" int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, voi
 
 extern "C" int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W, int C, void* dx,
                                   stf_stream_t stream) {
-  if (C % 8) return STF_EINVAL;
+  if (C % 8 || !argmax || !dout || !dx) return STF_EINVAL;     // the forward must have recorded the argmax
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long units = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(maxpool3_bwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,

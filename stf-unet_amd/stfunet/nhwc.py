@@ -460,13 +460,16 @@ def channel_sum(x: Feat, out):
 # ------------------------------------------------------------------ BatchNorm
 class BNState:
     """Per-forward BatchNorm quantities ([groups][C] each) kept for backward."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups")
+    __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups", "training")
 
-    def __init__(self, C, device, M, groups=1):
+    def __init__(self, C, device, M, groups=1, training=True):
         t = torch.empty(4, groups, C, dtype=torch.float32, device=device)
         self.mean, self.invstd, self.scale, self.shift = t.unbind(0)
         self.M = M
         self.groups = groups
+        # training: normalised with the batch statistics (mean / invstd above); eval:
+        # with the running statistics, which the backward treats as constants
+        self.training = training
 
     @staticmethod
     def identity(C, device):
@@ -521,7 +524,7 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
     """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats (its
     num_batches_tracked advances by ``groups`` at flush_batches_tracked())."""
     C = bn.num_features
-    st = BNState(C, bn.weight.device, M, groups)
+    st = BNState(C, bn.weight.device, M, groups, training)
     mom = 0.1 if bn.momentum is None else bn.momentum
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
@@ -621,6 +624,13 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
     C = y.C
     dev = y.buf.device
     G = st.groups
+    if st.training:
+        # the bias of a conv feeding a training-mode BatchNorm has gradient exactly 0:
+        # sum_m dy_m = gamma * invstd * (sum g - M mean(g) - mean(g xhat) sum xhat) and
+        # sum xhat = 0 over the normalised batch -- left at the zero of the fresh flat
+        # gradient instead of summing the rounded dy (the reference's autograd returns
+        # fp32 noise around 0 there)
+        dbias = None
     coef = torch.empty(G * 3 * C, dtype=torch.float32, device=dev)
     if G > 1 and (dgamma is not None or dbeta is not None):
         # grouped: the per-group sums stay parked; flush_bn_grads() adds them up for
@@ -630,6 +640,13 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         dgamma = dbeta = None
     call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, _p(bn.weight.detach()), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
+    if not st.training:
+        # eval mode (running statistics are constants): dy = gamma * invstd * g, i.e. the
+        # apply pass's dy = A g + B y + C with B = C = 0; dgamma = sum g xhat and
+        # dbeta = sum g come out of the same partial sums as in training mode
+        cv = coef.view(G, 3, C)
+        cv[:, 0].copy_(bn.weight.detach() * st.invstd)
+        cv[:, 1:].zero_()
     bpart = None
     if dbias is not None:
         bpart = torch.empty(_lib.load().stf_bn_bwd_apply_tiles(y.M, C) * C, dtype=torch.float32, device=dev)

@@ -357,7 +357,8 @@ class STFProgram:
         nhwc.bn_act(y0, S.bn0, a0)
         h4, w4 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
         p0 = new_feat(N, h4, w4, 64, dev)
-        S.pool_arg = torch.empty(N * h4 * w4 * 64, dtype=torch.uint8, device=dev) if training else None
+        # the window argmax the backward routes through (eval-mode backward needs it too)
+        S.pool_arg = torch.empty(N * h4 * w4 * 64, dtype=torch.uint8, device=dev) if need_bwd else None
         call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), _p(S.pool_arg), stream())
         S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
         # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat);

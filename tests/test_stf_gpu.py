@@ -338,3 +338,38 @@ def test_lstm_whole_sequence_equals_per_step(monkeypatch, T, B, H):
         out[mode] = [hT.dense(), st.c, lbuf.buf.clone(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
     for a, b in zip(out["0"], out["1"]):
         assert torch.equal(a, b)
+
+
+def test_stf_eval_mode_backward_vs_oracle():
+    """Whole-model STF backward in eval mode (BatchNorm with running statistics) vs autograd
+    of the fp32 oracle: with constant statistics the bf16 error stays small, so the
+    gradients are compared directly (within 2x the bf16 emulation's error + 0.02)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    g = np.load(os.path.join(GOLDEN, "stf_t4.npz"))
+    m = STFLSTMUNet(time_steps=4)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    gen = torch.Generator().manual_seed(3)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.2 - 0.1
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.5 + 0.75
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["target"])
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    o_loss.criterion(o_stf.forward(p, x, False)["out"], t).backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.bfloat16):
+        o_loss.criterion(o_emu.forward(pe, x, False)["out"], t).backward()
+    criterion({"out": m(x.to(DEV))["out"]}, t.to(DEV)).backward()
+    bad = []
+    for k, prm in m.named_parameters():
+        e_hip, e_emu = rel(prm.grad, p[k].grad), rel(pe[k].grad, p[k].grad)
+        if e_hip > 2 * e_emu + 0.02:
+            bad.append((k, e_hip, e_emu))
+    assert not bad, bad

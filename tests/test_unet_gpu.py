@@ -236,3 +236,45 @@ def test_checkpoint_resume_bitwise():
     for k, v in want.items():
         assert torch.equal(got[k], v), k
     assert sched2.get_last_lr() == sched.get_last_lr()
+
+
+def test_unet_eval_mode_backward_vs_oracle():
+    """Backward through eval-mode BatchNorm (running statistics are constants: dy = gamma *
+    invstd * g, conv biases get sum(dy) != 0) vs autograd of the fp32 oracle in eval mode;
+    gradients within 2x the bf16-storage emulation's error + 0.02 (no batch-statistics
+    amplification here).  Training-mode BN-fed conv biases: exactly 0."""
+    from stfunet.loss import criterion
+    model, sd = _model(8, seed=4)
+    gen = torch.Generator().manual_seed(5)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) - 0.5
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) + 0.5
+    model.load_state_dict(sd)
+    x5, t = dce_case(6, 2, 8, 64, 64)
+    x = x5.flatten(1, 2)
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref = o_unet.forward(p, x, training=False)["out"]
+    o_loss.criterion(ref, t).backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    o_loss.criterion(o_unet_bf16.forward(pe, x, training=False)["out"], t).backward()
+    model.eval()
+    out = model(x.to(DEV))["out"]
+    criterion({"out": out}, t.to(DEV)).backward()
+    assert rel(out.detach(), ref.detach()) < 1e-2
+    bad = []
+    for k, prm in model.named_parameters():
+        e_hip, e_emu = rel(prm.grad, p[k].grad), rel(pe[k].grad, p[k].grad)
+        if e_hip > 2 * e_emu + 0.02:
+            bad.append((k, e_hip, e_emu))
+    assert not bad, bad
+    for k, v in model.state_dict().items():                 # eval never moves the statistics
+        assert torch.equal(v.cpu(), sd[k]), k
+    model.train()
+    model.zero_grad()
+    out = model(x.to(DEV))["out"]
+    criterion({"out": out}, t.to(DEV)).backward()
+    for k, prm in model.named_parameters():
+        if _bn_fed_bias(k):
+            assert torch.count_nonzero(prm.grad) == 0, k
