@@ -563,6 +563,9 @@ class STFProgram:
 class _STFFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, prog, storage, *params):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("stfunet.STFLSTMUNet computes parameter gradients only; the input "
+                                      "sequence must not require grad")
         need_bwd = any(ctx.needs_input_grad[3:])
         with _lib.storage(storage):
             logits, saved = prog.forward(x, prog.m.training, need_bwd)

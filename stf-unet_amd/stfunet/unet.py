@@ -128,6 +128,9 @@ class UNetProgram:
         # finishes blocks in exactly the reverse of registration (= flat) order, so the
         # finished gradients always form a suffix of the flat buffer (DDP buckets).
         self.grad_ready_hook = None
+        # set by _UNetFunction for the backward in flight: also return d(loss)/d(input)
+        self.want_dx = False
+        self.dx = None
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
@@ -260,15 +263,21 @@ class UNetProgram:
             lvl = self.levels[j]
             C = lvl.cout
             dskip = dcats[j].slice(C, C)
-            dpool = lvl.backward(S.enc[j], self.flat, j > 0, dz=dskip, dpool=dpool)
+            dpool = lvl.backward(S.enc[j], self.flat, j > 0 or self.want_dx, dz=dskip, dpool=dpool)
             dcats[j] = None
             self._done(lvl.blk)
+        if self.want_dx:     # enc1's input gradient, NHWC 16-bit -> the input's [N, C, H, W] fp32
+            self.dx = dpool.dense()[:, : m.in_channels].contiguous()
 
 
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, prog, storage, *params):
-        need_bwd = any(ctx.needs_input_grad[3:])
+        ctx.need_dx = ctx.needs_input_grad[0]
+        if ctx.need_dx and prog.m.in_channels % 8:
+            raise NotImplementedError("input gradients need in_channels % 8 == 0 (the input is not "
+                                      "channel-padded then)")
+        need_bwd = any(ctx.needs_input_grad[3:]) or ctx.need_dx
         with _lib.storage(storage):
             logits, saved = prog.forward(x, prog.m.training, need_bwd)
         ctx.storage = storage
@@ -281,12 +290,17 @@ class _UNetFunction(torch.autograd.Function):
         prog = ctx.prog
         dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
-        with _lib.storage(ctx.storage):
-            prog.backward(ctx.saved, dlogits)
+        prog.want_dx, prog.dx = ctx.need_dx, None
+        try:
+            with _lib.storage(ctx.storage):
+                prog.backward(ctx.saved, dlogits)
+        finally:
+            prog.want_dx = False
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0)
-        return (None, None, None, *prog.flat.grad_views())
+        dx, prog.dx = prog.dx, None
+        return (dx, None, None, *prog.flat.grad_views())
 
 
 class UNet(nn.Module):

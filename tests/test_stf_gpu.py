@@ -373,3 +373,11 @@ def test_stf_eval_mode_backward_vs_oracle():
         if e_hip > 2 * e_emu + 0.02:
             bad.append((k, e_hip, e_emu))
     assert not bad, bad
+
+
+def test_stf_input_gradient_rejected():
+    from stfunet import STFLSTMUNet
+    m = STFLSTMUNet(time_steps=2).to(DEV)
+    x = torch.randn(1, 2, 1, 64, 64, device=DEV, requires_grad=True)
+    with pytest.raises(NotImplementedError):
+        m(x)

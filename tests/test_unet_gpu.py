@@ -278,3 +278,32 @@ def test_unet_eval_mode_backward_vs_oracle():
     for k, prm in model.named_parameters():
         if _bn_fed_bias(k):
             assert torch.count_nonzero(prm.grad) == 0, k
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_unet_input_gradient_vs_oracle(train):
+    """d(loss)/d(input) (autograd of the input tensor, e.g. saliency maps) vs the fp32
+    oracle, within 2x the bf16-storage emulation's error + 0.03; the parameter gradients
+    of the same backward are unchanged by asking for it."""
+    from stfunet.loss import criterion
+    model, sd = _model(8, seed=6)
+    x5, t = dce_case(7, 2, 8, 64, 64)
+    x = x5.flatten(1, 2)
+    res = []
+    for fwd in (o_unet.forward, o_unet_bf16.forward):
+        p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+        xr = x.clone().requires_grad_()
+        o_loss.criterion(fwd(p, xr, training=train)["out"], t).backward()
+        res.append(xr.grad)
+    model.train(train)
+    xg = x.to(DEV).requires_grad_()
+    criterion({"out": model(xg)["out"]}, t.to(DEV)).backward()
+    assert xg.grad is not None and xg.grad.shape == x.shape and xg.grad.dtype == torch.float32
+    e_hip, e_emu = rel(xg.grad, res[0]), rel(res[1], res[0])
+    assert e_hip <= 2 * e_emu + 0.03, (e_hip, e_emu)
+    g_with = {k: v.grad.clone() for k, v in model.named_parameters()}
+    model.load_state_dict(sd)
+    model.zero_grad()
+    criterion({"out": model(x.to(DEV))["out"]}, t.to(DEV)).backward()
+    for k, v in model.named_parameters():
+        assert torch.equal(v.grad, g_with[k]), k
