@@ -307,3 +307,36 @@ def test_unet_input_gradient_vs_oracle(train):
     criterion({"out": model(x.to(DEV))["out"]}, t.to(DEV)).backward()
     for k, v in model.named_parameters():
         assert torch.equal(v.grad, g_with[k]), k
+
+
+def test_gradient_accumulation_without_zero_grad():
+    """Two backward passes without zero_grad accumulate (p.grad = g_a + g_b, as autograd
+    does for nn.Modules), and stfunet's AdamW steps on the accumulated gradients exactly
+    like torch.optim.AdamW(fused=False) on copies of them."""
+    from stfunet.loss import criterion
+    from stfunet.optim import AdamW
+    model, sd = _model(8, seed=8)
+    model.train()
+    xa5, ta = dce_case(8, 2, 8, 64, 64)
+    xb5, tb = dce_case(9, 2, 8, 64, 64)
+    xa, xb = xa5.flatten(1, 2).to(DEV), xb5.flatten(1, 2).to(DEV)
+    ta, tb = ta.to(DEV), tb.to(DEV)
+    single = []
+    for x, t in ((xa, ta), (xb, tb)):
+        model.load_state_dict(sd)
+        model.zero_grad(set_to_none=True)
+        criterion({"out": model(x)["out"]}, t).backward()
+        single.append({k: v.grad.clone() for k, v in model.named_parameters()})
+    model.load_state_dict(sd)
+    model.zero_grad(set_to_none=True)
+    criterion({"out": model(xa)["out"]}, ta).backward()
+    criterion({"out": model(xb)["out"]}, tb).backward()
+    for k, v in model.named_parameters():
+        assert torch.equal(v.grad, single[0][k] + single[1][k]), k
+    ref = {k: v.detach().clone().requires_grad_() for k, v in model.named_parameters()}
+    for k in ref:
+        ref[k].grad = dict(model.named_parameters())[k].grad.clone()
+    AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4).step()
+    torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=1e-4, foreach=False).step()
+    for k, v in model.named_parameters():
+        assert torch.allclose(v.detach(), ref[k].detach(), rtol=0, atol=1e-6), k
