@@ -220,3 +220,46 @@ def test_stf_fullsize_train_vs_fp32(T):
     assert abs(loss.item() - ref_loss) < 0.03
     for k, p in m.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
+    """configs[2] (T=8, B=16, 256^2): whole-model STF gradients at the benchmarked size.
+    With running statistics (eval-mode BatchNorm) the 16-bit rounding is not amplified, so
+    every parameter gradient -- stem, the 16 ResNet blocks, the four per-pixel LSTMs, the
+    decoder and head -- is compared with autograd of the fp32 restatement: rel-L2 within
+    2x the bf16 emulation's error + 0.02 (as test_stf_eval_mode_backward_vs_oracle at T=4)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    gen = torch.Generator().manual_seed(3)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.2 - 0.1
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.5 + 0.75
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = dce_batch(16, 8, 256, 256, seed=11, device=DEV, mask_hw=(128, 128))
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref_loss = o_loss.criterion(o_stf.forward(p, x, False)["out"], t)
+    ref_loss.backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.bfloat16):
+        o_loss.criterion(o_emu.forward(pe, x, False)["out"], t).backward()
+    loss = criterion({"out": m(x)["out"]}, t)
+    loss.backward()
+    assert abs(loss.item() - ref_loss.item()) < 1e-2, (loss.item(), ref_loss.item())
+    bad, worst = [], (-1.0, 0.0, 0.0, "")
+    for k, prm in m.named_parameters():
+        e_hip, e_emu = rel(prm.grad, p[k].grad), rel(pe[k].grad, p[k].grad)
+        if e_hip > 2 * e_emu + 0.02:
+            bad.append((k, e_hip, e_emu))
+        worst = max(worst, (e_hip / (2 * e_emu + 0.02), e_hip, e_emu, k))
+    print(f"\nSTF cfg3 eval-mode backward: loss {loss.item():.6f} vs {ref_loss.item():.6f}, tightest gradient "
+          f"{worst[3]}: rel {worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
+    assert not bad, bad
