@@ -263,3 +263,37 @@ def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
     print(f"\nSTF cfg3 eval-mode backward: loss {loss.item():.6f} vs {ref_loss.item():.6f}, tightest gradient "
           f"{worst[3]}: rel {worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
     assert not bad, bad
+
+
+def test_stf_cfg5_fullsize_eval_fp16_vs_fp32():
+    """configs[4]'s per-sample shape (512^2, T=32 DCE frames + 3 PK maps, fp16 storage = the
+    reference's --amp numerics), eval mode with fixed running statistics: PK fusion at every
+    scale, the 4-channel stem, the T=32 LSTMs and the decoder against the fp32 restatement,
+    logits rel-L2 within 2x the fp16-storage emulation's error + 2e-4 (B = 1 bounds the fp32
+    reference's memory)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=32, use_pk_maps=True)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    gen = torch.Generator().manual_seed(4)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.2 - 0.1
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.5 + 0.75
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    m.storage_dtype = torch.float16
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, _ = dce_batch(1, 32, 512, 512, seed=12, device=DEV, pk_channels=3, mask_hw=(256, 256))
+    with torch.no_grad():
+        out = m(x)["out"].float()
+        ref = o_stf.forward(sd, x, False, use_pk_maps=True)["out"]
+        with o_q.storage(torch.float16):
+            emu = o_emu.forward(sd, x, False, use_pk_maps=True)["out"]
+    assert out.shape == (1, 2, 256, 256)
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    print(f"\nSTF cfg5 (512^2, T=32 + PK, fp16) eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
+    assert e_hip <= 2 * e_emu + 2e-4, (e_hip, e_emu)
