@@ -205,10 +205,14 @@ def call(name, *args):
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
+_get_device = torch._C._cuda_getDevice
+
+
 def stream():
-    """Raw hipStream_t of torch's current stream on the current device (the raw
-    accessor skips torch.cuda.current_stream()'s Python wrapper: ~9 us -> <1 us per
-    launch, and the STF step is host-bound with ~180 launches from Python)."""
+    """Raw hipStream_t of torch's current stream on the current device, as a plain int
+    (every entry point declares its stream argument c_void_p, which ctypes fills from an
+    int; the raw accessor skips torch.cuda.current_stream()'s Python wrapper: ~9 us ->
+    <1 us per launch, and the STF step is host-bound with ~600 launches from Python)."""
     if _raw_stream is not None:
-        return ctypes.c_void_p(_raw_stream(torch._C._cuda_getDevice()))
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        return _raw_stream(_get_device())
+    return torch.cuda.current_stream().cuda_stream

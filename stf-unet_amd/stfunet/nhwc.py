@@ -27,7 +27,10 @@ def sdt():
 
 
 def _p(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    """Device address of ``t`` (None -> NULL) as an int: the entry points declare their
+    pointer arguments c_void_p and the descriptor structs c_void_p fields, which ctypes
+    fills from ints (no c_void_p object per argument on the launch path)."""
+    return t.data_ptr() if t is not None else None
 
 
 class KernelTimer:
@@ -134,15 +137,16 @@ class Feat:
         return self.N * self.H * self.W
 
     def ptr(self):
-        return ctypes.c_void_p(self.buf.data_ptr() + 2 * self.off)
+        return self.buf.data_ptr() + 2 * self.off
 
     def slice(self, c0, c):
         assert 0 <= c0 and c0 + c <= self.C
         return Feat(self.buf, self.N, self.H, self.W, c, self.cs, self.off + c0)
 
     def check(self):
-        assert self.buf.dtype == sdt() and self.buf.is_cuda
-        assert self.buf.numel() >= self.M * self.cs, "feature buffer too small"
+        b = self.buf
+        assert b.dtype == _lib._active and b.is_cuda
+        assert b.numel() >= self.N * self.H * self.W * self.cs, "feature buffer too small"
         assert self.off + self.C <= self.cs
 
     def dense(self):
@@ -232,12 +236,13 @@ class PackCache:
         self.fresh = set(self.recorded)
 
     def get(self, w, mode, cpad):
-        self._match_storage()
-        w = w.detach()
-        key = (w.data_ptr(), tuple(w.shape), mode, cpad)
+        if self.dtype is not _lib._active:
+            self._match_storage()
+        key = (w.data_ptr(), w.shape, mode, cpad)
         self.seen[key] = None
         ent = self.bufs.get(key)
         if ent is None:
+            w = w.detach()
             ent = self.bufs[key] = (w, _pack_into(w, mode, cpad, None, launch=False), mode, cpad)
         if key not in self.fresh:
             _pack_into(w, mode, cpad, ent[1])
@@ -274,6 +279,20 @@ def pack_weight(w, mode, cpad=0):
 
 
 # ------------------------------------------------------------------ implicit GEMM
+_QUERIES = {}    # igemm launch signature -> (statistics / BN-backward tiles, split-K workspace bytes)
+_PLANS = {}      # wgrad launch signature -> (splits, workspace bytes)
+
+
+def _ws_bytes_with(a, want_stats):
+    """stf_igemm_ws_bytes with the statistics pointer set (non-NULL) as it will be at launch."""
+    if want_stats:
+        a.stats = 16
+    try:
+        return _lib.load().stf_igemm_ws_bytes(ctypes.byref(a))
+    finally:
+        a.stats = None
+
+
 def _geom(src: Feat, Hd, Wd, R, S, stride, pad, transposed):
     return ConvGeom(src.N, src.H, src.W, src.C, src.cs, Hd, Wd, R, S, stride, pad, int(transposed))
 
@@ -296,9 +315,16 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         # every gathered tap must stay inside (or be zero padding of) the source
         assert (Hd - 1) * stride - pad + R - 1 <= src.H - 1 + pad
     M = src.N * Hd * Wd
-    a = IgemmArgs(_geom(src, Hd, Wd, R, S, stride, pad, transposed), src.ptr(), _p(wgt), nout, dst.ptr(),
+    dptr = dst.ptr()
+    a = IgemmArgs(_geom(src, Hd, Wd, R, S, stride, pad, transposed), src.ptr(), _p(wgt), nout, dptr,
                   dst.cs, _p(bias), None, int(scatter2x2), M // groups if groups > 1 else 0, int(accumulate),
                   ctypes.pointer(lstm) if lstm is not None else None)
+    # the size queries below are pure functions of the launch signature (geometry, flags,
+    # which optional pointers are set, the destination's 16-B alignment): asked once each
+    qkey = (src.N, src.H, src.W, src.C, src.cs, Hd, Wd, R, S, stride, pad, transposed, nout, dst.cs,
+            bias is None, scatter2x2, groups, accumulate, None if lstm is None else lstm.backward,
+            bnr is not None, want_stats, dptr & 15)
+    q = _QUERIES.get(qkey)
     stats, tiles = None, 0
     if bnr is not None:
         y, st, relu = bnr
@@ -306,13 +332,21 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         assert not want_stats and st.groups == groups and (y.N, y.H, y.W, y.C) == (dst.N, dst.H, dst.W, dst.C)
         epi = BnrEpi(y.ptr(), y.cs, _p(st.scale), _p(st.shift), _p(st.mean), _p(st.invstd), int(relu), None)
         a.bnr = ctypes.pointer(epi)
-        tiles = _lib.load().stf_igemm_bnr_tiles(ctypes.byref(a))
+    if q is None:
+        lib = _lib.load()
+        tq = 0
+        if bnr is not None:
+            tq = lib.stf_igemm_bnr_tiles(ctypes.byref(a))
+        elif want_stats:
+            tq = lib.stf_igemm_stat_tiles(ctypes.byref(a))
+        q = _QUERIES[qkey] = (tq, _ws_bytes_with(a, want_stats))
+    tiles, nb = q
+    if bnr is not None:
         stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
-        epi.partial = _p(stats)
+        epi.partial = stats.data_ptr()
     if want_stats:
-        tiles = _lib.load().stf_igemm_stat_tiles(ctypes.byref(a))
         stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
-        a.stats = _p(stats)
+        a.stats = stats.data_ptr()
     t = TIMER
     if t is not None:
         name = _kernel_name("stf_igemm_kernel_name", ("i", src.N, src.H, src.W, src.C, Hd, Wd, nout, R, S, stride,
@@ -321,10 +355,9 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         if not t.wants(name):
             t = None
     ws = None
-    nb = _lib.load().stf_igemm_ws_bytes(ctypes.byref(a))
     if nb:
         ws = torch.empty(nb // 4, dtype=torch.float32, device=dst.buf.device)
-        a.ws = _p(ws)
+        a.ws = ws.data_ptr()
     ev = t.begin() if t is not None else None
     call("stf_igemm", ctypes.byref(a), stream())
     if t is not None:
@@ -378,7 +411,7 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
         # host fast path (the STF step issues ~55 of these and is host-bound): one pooled
         # event instead of wait_stream's fresh Event, torch's current stream switched by id
         main = WGRAD_MAIN
-        if main is None or _lib.stream().value != main.cuda_stream:   # e.g. called on another side stream
+        if main is None or _lib.stream() != main.cuda_stream:   # e.g. called on another side stream
             main = torch.cuda.current_stream()
         ev = _sync_event()
         ev.record(main)
@@ -432,12 +465,17 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
     assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == dy.C * x.C * R * S
     g = ConvGeom(x.N, x.H, x.W, x.C, x.cs, dy.H, dy.W, R, S, stride, pad, 0)
     a = WgradArgs(g, dy.ptr(), dy.cs, dy.C, x.ptr(), None, 0, grid_blocks)
-    splits = ctypes.c_int(0)
-    nbytes = ctypes.c_size_t(0)
-    call("stf_wgrad_plan", ctypes.byref(a), ctypes.byref(splits), ctypes.byref(nbytes))
-    ws = torch.empty(nbytes.value // 4, dtype=torch.float32, device=out.device)
-    a.ws = _p(ws)
-    a.splits = splits.value
+    pkey = (x.N, x.H, x.W, x.C, x.cs, dy.H, dy.W, dy.C, dy.cs, R, S, stride, pad, grid_blocks)
+    plan = _PLANS.get(pkey)
+    if plan is None:       # stf_wgrad_plan is a pure function of the geometry and grid request
+        splits = ctypes.c_int(0)
+        nbytes = ctypes.c_size_t(0)
+        call("stf_wgrad_plan", ctypes.byref(a), ctypes.byref(splits), ctypes.byref(nbytes))
+        plan = _PLANS[pkey] = (splits.value, nbytes.value)
+    splits, nbytes = plan
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
+    a.ws = ws.data_ptr()
+    a.splits = splits
     t = TIMER
     if t is not None:
         name = _kernel_name("stf_wgrad_kernel_name", ("w", x.N, x.H, x.W, x.C, dy.H, dy.W, dy.C, R, S, stride, pad), a)
@@ -447,7 +485,7 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
     call("stf_wgrad", ctypes.byref(a), stream())
     if t is not None:
         t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
-    call("stf_wgrad_reduce", _p(ws), splits.value, dy.C, R, S, x.C, _p(out), stream())
+    call("stf_wgrad_reduce", ws.data_ptr(), splits, dy.C, R, S, x.C, out.data_ptr(), stream())
 
 
 def channel_sum(x: Feat, out):
@@ -534,8 +572,8 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
         _RUN_PENDING.append((_RunDesc(stats.data_ptr(), rm.data_ptr(), rv.data_ptr(), M // groups, tiles, groups, C,
                                       float(mom)), stats))
         rm = rv = None
-    call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, _p(bn.weight.detach()),
-         _p(bn.bias.detach()), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
+    call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, bn.weight.data_ptr(),
+         bn.bias.data_ptr(), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
          _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
          stream())
     if training and bn.track_running_stats:
@@ -638,7 +676,7 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                         dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
         dgamma = dbeta = None
-    call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, _p(bn.weight.detach()), _p(st.mean),
+    call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     if not st.training:
         # eval mode (running statistics are constants): dy = gamma * invstd * g, i.e. the

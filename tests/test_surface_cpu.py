@@ -119,3 +119,40 @@ def test_product_synthetic_cases_match_fixture_generator():
     for seed in (0, 5, 2003):
         a, b = dce_case(seed, 2, 8, 32, 48), splitmix_dce_case(seed, 2, 8, 32, 48)
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_size_queries_depend_only_on_the_cached_signature():
+    """nhwc.igemm / nhwc._wgrad ask stf_igemm_stat_tiles / _bnr_tiles / _ws_bytes and
+    stf_wgrad_plan once per launch signature (geometry, flags, which optional pointers are
+    set, the destination's 16-B alignment) and reuse the answer: the C functions must not
+    look at anything else, e.g. the pointer values themselves (host-only calls, no GPU)."""
+    from stfunet import _lib
+    lib = _lib.load()
+    shapes = [  # N, Hs, Ws, Cs, Hd, Wd, R, S, stride, pad, transposed, Nout, groups
+        (64, 256, 256, 64, 256, 256, 3, 3, 1, 1, 0, 64, 1),       # halo, full resolution
+        (64, 16, 16, 512, 16, 16, 3, 3, 1, 1, 0, 1024, 1),         # 16^2 bottleneck
+        (128, 8, 8, 512, 8, 8, 3, 3, 1, 1, 0, 512, 8),             # STF layer4: split-K, grouped
+        (128, 16, 16, 256, 8, 8, 3, 3, 2, 1, 0, 512, 8),           # strided
+        (16, 8, 8, 512, 16, 16, 3, 3, 2, 1, 1, 256, 1),            # transposed gather
+        (64, 256, 256, 8, 256, 256, 3, 3, 1, 1, 0, 64, 1),         # 8-channel network input
+    ]
+    for N, Hs, Ws, Cs, Hd, Wd, R, S, st, pad, tr, nout, groups in shapes:
+        M = N * Hd * Wd
+        res = set()
+        for base in (1 << 32, (7 << 36) + 4096):
+            g = _lib.ConvGeom(N, Hs, Ws, Cs, Cs, Hd, Wd, R, S, st, pad, tr)
+            a = _lib.IgemmArgs(g, base, base + (1 << 30), nout, base + (2 << 30), nout, None, None, 0,
+                               M // groups if groups > 1 else 0, 0, None)
+            a.stats = base + (3 << 30)
+            q = (lib.stf_igemm_stat_tiles(ctypes.byref(a)), lib.stf_igemm_ws_bytes(ctypes.byref(a)))
+            epi = _lib.BnrEpi(base + (4 << 30), nout, base, base, base, base, 1, base)
+            a.stats = None
+            a.bnr = ctypes.pointer(epi)
+            q += (lib.stf_igemm_bnr_tiles(ctypes.byref(a)), lib.stf_igemm_ws_bytes(ctypes.byref(a)))
+            if not tr and Cs % 64 == 0 and nout % 64 == 0:
+                w = _lib.WgradArgs(g, base, nout, nout, base + (1 << 30), None, 0, 0)
+                sp, nb = ctypes.c_int(0), ctypes.c_size_t(0)
+                assert lib.stf_wgrad_plan(ctypes.byref(w), ctypes.byref(sp), ctypes.byref(nb)) == 0
+                q += (sp.value, nb.value)
+            res.add(q)
+        assert len(res) == 1, (N, Hs, Cs, nout, res)
