@@ -222,8 +222,10 @@ def test_stf_fullsize_train_vs_fp32(T):
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
 
 
-def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
-    """configs[2] (T=8, B=16, 256^2): whole-model STF gradients at the benchmarked size.
+@pytest.mark.parametrize("T", [8, 16])
+def test_stf_fullsize_eval_backward_vs_fp32(T):
+    """configs[2] (T=8) and configs[3]'s per-GPU workload (T=16), B=16, 256^2: whole-model
+    STF gradients at the benchmarked sizes.
     With running statistics (eval-mode BatchNorm) the 16-bit rounding is not amplified, so
     every parameter gradient -- stem, the 16 ResNet blocks, the four per-pixel LSTMs, the
     decoder and head -- is compared with autograd of the fp32 restatement: rel-L2 within
@@ -233,7 +235,7 @@ def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
     from stfunet import STFLSTMUNet
     from stfunet.loss import criterion
     from stfunet.synthetic import dce_batch
-    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8)
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
     sd = canonical_state_dict(m.state_dict(), seed=0)
     gen = torch.Generator().manual_seed(3)
     for k, v in sd.items():
@@ -244,7 +246,7 @@ def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
     m.load_state_dict(sd)
     m = m.to(DEV).eval()
     sd = {k: v.to(DEV) for k, v in sd.items()}
-    x, t = dce_batch(16, 8, 256, 256, seed=11, device=DEV, mask_hw=(128, 128))
+    x, t = dce_batch(16, T, 256, 256, seed=11, device=DEV, mask_hw=(128, 128))
     p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     ref_loss = o_loss.criterion(o_stf.forward(p, x, False)["out"], t)
     ref_loss.backward()
@@ -260,7 +262,7 @@ def test_stf_cfg3_fullsize_eval_backward_vs_fp32():
         if e_hip > 2 * e_emu + 0.02:
             bad.append((k, e_hip, e_emu))
         worst = max(worst, (e_hip / (2 * e_emu + 0.02), e_hip, e_emu, k))
-    print(f"\nSTF cfg3 eval-mode backward: loss {loss.item():.6f} vs {ref_loss.item():.6f}, tightest gradient "
+    print(f"\nSTF T={T} eval-mode backward: loss {loss.item():.6f} vs {ref_loss.item():.6f}, tightest gradient "
           f"{worst[3]}: rel {worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
     assert not bad, bad
 
