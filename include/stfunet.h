@@ -284,6 +284,15 @@ int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n, float lr,
  * computes them for stf_adamw. */
 int stf_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
                   float beta1, float beta2, float eps, float weight_decay, stf_stream_t stream);
+/* AdamW under torch.amp.GradScaler without a host sync (the optimizer advertises
+ * _step_supports_amp_scaling, as torch's fused AdamW does, which the reference builds with
+ * fused=True, train.py:230-237): grad_scale = DEVICE scale the gradients carry (NULL:
+ * already unscaled; multiplied by 1/scale in fp32 = GradScaler.unscale_'s arithmetic),
+ * found_inf = DEVICE flag, != 0 skips the update and leaves hyper[1] (the step count)
+ * unchanged; otherwise hyper[1] += 1 and the update is stf_adamw_dev's. */
+int stf_adamw_amp(float* p, const float* g, float* m, float* v, int64_t n, float* hyper,
+                  const float* grad_scale, const float* found_inf, float beta1, float beta2, float eps,
+                  float weight_decay, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- layout
  * x [N][C][H][W] fp32 -> NHWC bf16 with Cpad (>= C, multiple of 8) channels,

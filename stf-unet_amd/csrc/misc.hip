@@ -229,16 +229,23 @@ long grid_for(long units, long cap) {
 // be replayed with the schedule's new lr (written between replays) and a step count
 // that advances on the device.  Bias corrections in double, rounded to fp32 exactly as
 // the host computes them for stf_adamw, so both paths produce the same bits.
+// GradScaler (amp) variant: gradients arrive scaled by *gscale (NULL: already unscaled)
+// and are multiplied by 1/*gscale in fp32 -- GradScaler.unscale_'s arithmetic, exact for
+// its power-of-two scales; *finf != 0 (an inf/nan gradient) skips the whole update, like
+// torch's fused AdamW under GradScaler, with no host synchronisation.
 __global__ void adamw_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                  float* __restrict__ v, long n, const float* __restrict__ hyper, float b1, float b2,
-                                 float eps, float wd) {
+                                 float eps, float wd, const float* __restrict__ gscale,
+                                 const float* __restrict__ finf) {
+  if (finf && finf[0] != 0.f) return;
+  const float inv = gscale ? 1.f / gscale[0] : 1.f;
   const float lr = hyper[0];
   const double step = hyper[1];
   const float bc1 = (float)(1.0 - pow((double)b1, step)), bc2 = (float)(1.0 - pow((double)b2, step));
   const float step_size = lr / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
     float pp = p[i] * (1.f - lr * wd);
-    const float gg = g[i];
+    const float gg = gscale ? g[i] * inv : g[i];
     const float mm = m[i] + (1.f - b1) * (gg - m[i]);
     const float ww = b2 * v[i] + (1.f - b2) * gg * gg;
     pp -= step_size * mm / (sqrtf(ww) * inv_sqrt_bc2 + eps);
@@ -248,12 +255,30 @@ __global__ void adamw_dev_kernel(float* __restrict__ p, const float* __restrict_
   }
 }
 
+// the device step count advances unless the update is skipped (one lane; vector stores)
+__global__ void adamw_amp_step_kernel(float* __restrict__ hyper, const float* __restrict__ finf) {
+  if (threadIdx.x == 0 && !(finf && finf[0] != 0.f)) hyper[1] += 1.f;
+}
+
 extern "C" int stf_adamw_dev(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper, float beta1,
                              float beta2, float eps, float weight_decay, stf_stream_t stream) {
   if (n < 0 || !hyper) return STF_EINVAL;
   if (n == 0) return 0;
   hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 4096)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (long)n,
-                     hyper, beta1, beta2, eps, weight_decay);
+                     hyper, beta1, beta2, eps, weight_decay, nullptr, nullptr);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_adamw_amp(float* p, const float* g, float* m, float* v, int64_t n, float* hyper,
+                             const float* grad_scale, const float* found_inf, float beta1, float beta2, float eps,
+                             float weight_decay, stf_stream_t stream) {
+  if (n < 0 || !hyper || !found_inf) return STF_EINVAL;
+  hipLaunchKernelGGL(adamw_amp_step_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, hyper, found_inf);
+  STF_CHECK_LAUNCH();
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adamw_dev_kernel, dim3(grid_for(n, 4096)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v, (long)n,
+                     hyper, beta1, beta2, eps, weight_decay, grad_scale, found_inf);
   STF_CHECK_LAUNCH();
   return 0;
 }
@@ -336,7 +361,7 @@ extern "C" const char* stf_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-extern "C" int stf_abi_version(void) { return 7; }
+extern "C" int stf_abi_version(void) { return 8; }
 
 extern "C" int stf_storage_type(void) {
 #ifdef STF_FP16

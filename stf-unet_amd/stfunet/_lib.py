@@ -88,6 +88,7 @@ _SIGS = {
     "stf_adamw": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_float, c_float, c_float,
                           P]),
     "stf_adamw_dev": (c_int, [P, P, P, P, c_int64, P, c_float, c_float, c_float, c_float, P]),
+    "stf_adamw_amp": (c_int, [P, P, P, P, c_int64, P, P, P, c_float, c_float, c_float, c_float, P]),
     "stf_pack_input": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_pack_weights": (c_int, [P, c_int, c_int64, P]),

@@ -10,7 +10,16 @@ When the parameters are exactly one model's ``FlatParams`` and their ``.grad``
 tensors are the flat gradient views written by backward, the update is one
 ``stf_adamw`` launch over the whole buffer; otherwise gradients are first packed
 into a flat scratch (one copy) and the same kernel runs.
+
+Under ``torch.amp.GradScaler`` (the reference's ``--amp`` step, train_and_eval.py:396-404)
+the optimizer takes the scaler's device-side scale and inf flag (``stf_adamw_amp``)
+instead of letting the scaler unscale the gradients and read ``found_inf`` on the host:
+the contract torch's fused AdamW implements, so the gradients stay scaled after
+``step()`` exactly as with the reference's ``AdamW(fused=True)``, and the step costs no
+host synchronisation.
 """
+import os
+
 import torch
 
 from ._lib import call, stream
@@ -22,6 +31,11 @@ def _align4(n):
 
 
 class AdamW(torch.optim.Optimizer):
+    # torch/amp/grad_scaler.py GradScaler.step: an optimizer advertising this receives
+    # ``grad_scale`` / ``found_inf`` (device tensors) as attributes for the step
+    # (STF_AMP_DEVICE_STEP=0: the scaler's own unscale_ + host inf check, for A/B)
+    _step_supports_amp_scaling = os.environ.get("STF_AMP_DEVICE_STEP", "1") != "0"
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, fused=None,
                  capturable=False, **unused):
         """``capturable=True``: lr and the step count live on the device ({lr, step}
@@ -110,6 +124,11 @@ class AdamW(torch.optim.Optimizer):
                 raise RuntimeError("stfunet.optim.AdamW runs on the gfx950 kernel only (no CPU fallback)")
             fb = self._group_buffers(gi, group)
             b1, b2 = group["betas"]
+            found_inf = getattr(self, "found_inf", None)
+            if found_inf is not None:
+                self._amp_step(gi, group, params, fb, getattr(self, "grad_scale", None), found_inf)
+                continue
+            self._sync_host_step(gi, fb)
             if self.capturable:
                 h = self._hyper_of(gi, group, fb)
                 if not torch.cuda.is_current_stream_capturing():
@@ -139,6 +158,44 @@ class AdamW(torch.optim.Optimizer):
                 for p, o in zip(params, fb["offs"]):
                     p.copy_(pf[o:o + p.numel()].view_as(p))
         return loss
+
+    def _amp_step(self, gi, group, params, fb, grad_scale, found_inf):
+        """GradScaler step: unscale (x 1/scale) and the inf skip inside the kernel, the step
+        count advanced on the device (host mirror refreshed lazily, _sync_host_step)."""
+        b1, b2 = group["betas"]
+        dev = fb["m"].device
+        h = self._hyper_of(gi, group, fb)
+        if not fb.get("dev_step"):          # the host mirror was authoritative until now
+            h[1:2].fill_(float(fb["step"]))
+        h[0:1].fill_(float(group["lr"]))
+        fb["dev_step"] = True
+        if grad_scale is not None and not torch.is_tensor(grad_scale):
+            grad_scale = torch.full((1,), float(grad_scale), dtype=torch.float32, device=dev)
+        gsc = grad_scale.to(device=dev, dtype=torch.float32) if grad_scale is not None else None
+        fin = found_inf.to(device=dev, dtype=torch.float32)
+        g = self._flat_grad(params, fb)
+        pf = fb["p"]
+        if pf is None:       # scattered parameters: gather, update (or skip), scatter back
+            pf = torch.zeros(fb["n"], dtype=torch.float32, device=dev)
+            for p, o in zip(params, fb["offs"]):
+                pf[o:o + p.numel()].copy_(p.reshape(-1))
+        call("stf_adamw_amp", _p(pf), _p(g), _p(fb["m"]), _p(fb["v"]), fb["n"], _p(h), _p(gsc), _p(fin),
+             float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]), stream())
+        if fb["p"] is None:
+            for p, o in zip(params, fb["offs"]):
+                p.copy_(pf[o:o + p.numel()].view_as(p))
+
+    def _sync_host_step(self, gi, fb):
+        """After GradScaler steps the device count is authoritative (a skipped step does not
+        advance it): copy it to the host mirror before a host-scalar step or a state_dict."""
+        if fb.get("dev_step"):
+            fb["step"].fill_(float(self._hyper[gi][1].item()))
+            fb["dev_step"] = False
+
+    def state_dict(self):
+        for gi, fb in self._flat.items():
+            self._sync_host_step(gi, fb)
+        return super().state_dict()
 
     def _flat_grad(self, params, fb):
         g0 = params[0].grad

@@ -340,3 +340,51 @@ def test_gradient_accumulation_without_zero_grad():
     torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=1e-4, foreach=False).step()
     for k, v in model.named_parameters():
         assert torch.allclose(v.detach(), ref[k].detach(), rtol=0, atol=1e-6), k
+
+
+def test_gradscaler_step_on_device_and_inf_skip():
+    """Under GradScaler the optimizer takes the scaler's device scale and inf flag
+    (_step_supports_amp_scaling, like the reference's AdamW(fused=True)): the update equals
+    torch.optim.AdamW on the unscaled gradients, the gradients stay scaled after step(), an
+    inf gradient skips the update and the step count, and the scaler backs off."""
+    from stfunet.loss import criterion
+    from stfunet.optim import AdamW
+    model, _ = _model(8, seed=11)
+    model.train()
+    x5, t = dce_case(12, 2, 8, 64, 64)
+    x, t = x5.flatten(1, 2).to(DEV), t.to(DEV)
+    opt = AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    scaler = torch.amp.GradScaler("cuda")
+    named = dict(model.named_parameters())
+
+    def backward():
+        opt.zero_grad()
+        scaler.scale(criterion({"out": model(x)["out"]}, t)).backward()
+
+    # 1) an inf gradient: nothing moves, the step count stays 0, the scale halves
+    backward()
+    before = {k: v.detach().clone() for k, v in named.items()}
+    named["out_conv.weight"].grad.view(-1)[0] = float("inf")
+    scaler.step(opt)
+    scaler.update()
+    assert scaler.get_scale() == 32768.0
+    for k, v in named.items():
+        assert torch.equal(v.detach(), before[k]), k
+    assert int(opt.state_dict()["state"][0]["step"]) == 0
+    # 2) a finite step: torch.optim.AdamW on the unscaled copies, step count 1
+    backward()
+    scaled = {k: v.grad.clone() for k, v in named.items()}
+    ref = {k: v.detach().clone().requires_grad_() for k, v in named.items()}
+    for k in ref:
+        ref[k].grad = scaled[k] / 32768.0
+    scaler.step(opt)
+    scaler.update()
+    torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=1e-4, foreach=False).step()
+    for k, v in named.items():
+        assert torch.equal(v.grad, scaled[k]), k                 # still scaled, as with fused AdamW
+        assert torch.allclose(v.detach(), ref[k].detach(), rtol=0, atol=1e-6), k
+    assert int(opt.state_dict()["state"][0]["step"]) == 1
+    # 3) a plain (unscaled) step afterwards continues the count on the host path
+    backward()
+    opt.step()
+    assert int(opt.state_dict()["state"][0]["step"]) == 2
