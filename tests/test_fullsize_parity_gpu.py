@@ -299,3 +299,48 @@ def test_stf_cfg5_fullsize_eval_fp16_vs_fp32():
     e_hip, e_emu = rel(out, ref), rel(emu, ref)
     print(f"\nSTF cfg5 (512^2, T=32 + PK, fp16) eval: logits rel {e_hip:.3e} (emu {e_emu:.3e})")
     assert e_hip <= 2 * e_emu + 2e-4, (e_hip, e_emu)
+
+
+def test_stf_cfg3_fullsize_train_fp16_gradients_vs_fp32():
+    """configs[2]'s shape in the reference's --amp numerics (fp16 storage, the loss scaled by
+    GradScaler's initial 65536 before backward so per-pixel gradients stay clear of fp16's
+    subnormal range), TRAIN mode (batch statistics): fp16 keeps 3 more mantissa bits than
+    bf16, so the whole-model gradients are compared with autograd of the fp32 restatement --
+    each within 2x the fp16-storage emulation's error + 0.03 (the UNet cfg2 rule), loss
+    within 2x the emulation's + 1e-4."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    m.storage_dtype = torch.float16
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = dce_batch(16, 8, 256, 256, seed=13, device=DEV, mask_hw=(128, 128))
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref_loss = o_loss.criterion(o_stf.forward(p, x, True)["out"], t)
+    ref_loss.backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.float16):
+        emu_loss = o_loss.criterion(o_emu.forward(pe, x, True)["out"], t)
+        emu_loss.backward()
+    scale = 65536.0
+    loss = criterion({"out": m(x)["out"]}, t)
+    (loss * scale).backward()
+    assert abs(loss.item() - ref_loss.item()) <= 2 * abs(emu_loss.item() - ref_loss.item()) + 1e-4, \
+        (loss.item(), ref_loss.item(), emu_loss.item())
+    bad, worst, errs = [], (-1.0, 0.0, 0.0, ""), []
+    for k, prm in m.named_parameters():
+        e_hip, e_emu = rel(prm.grad / scale, p[k].grad), rel(pe[k].grad, p[k].grad)
+        errs.append(e_hip)
+        if e_hip > 2 * e_emu + 0.03:
+            bad.append((k, e_hip, e_emu))
+        worst = max(worst, (e_hip / (2 * e_emu + 0.03), e_hip, e_emu, k))
+    errs.sort()
+    print(f"\nSTF cfg3 train fp16: loss {loss.item():.6f} vs {ref_loss.item():.6f} (emu {emu_loss.item():.6f}), "
+          f"gradient rel median {errs[len(errs) // 2]:.3e}, tightest {worst[3]}: rel {worst[1]:.3e} "
+          f"(emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
+    assert not bad, bad
