@@ -52,11 +52,17 @@ def _unet(seed=0):
     return m.to(DEV), {k: v.to(DEV) for k, v in sd.items()}
 
 
-def _oracle_train(sd, x, t, fwd):
+def _oracle_train(sd, x, t, fwd, scale=1.0):
+    """fp32 / emulated forward + autograd; ``scale``: backward of loss * scale (GradScaler),
+    the gradients divided by it again."""
     p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     out = fwd(p, x, training=True)["out"]
     loss = o_loss.criterion(out, t)
-    loss.backward()
+    (loss * scale).backward()
+    if scale != 1.0:
+        for v in p.values():
+            if v.grad is not None:
+                v.grad.div_(scale)
     return p, out.detach(), loss.item()
 
 
@@ -324,10 +330,13 @@ def test_stf_cfg3_fullsize_train_fp16_gradients_vs_fp32():
     ref_loss = o_loss.criterion(o_stf.forward(p, x, True)["out"], t)
     ref_loss.backward()
     pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    scale = 65536.0
     with o_q.storage(torch.float16):
         emu_loss = o_loss.criterion(o_emu.forward(pe, x, True)["out"], t)
-        emu_loss.backward()
-    scale = 65536.0
+        (emu_loss * scale).backward()
+    for v in pe.values():
+        if v.grad is not None:
+            v.grad.div_(scale)
     loss = criterion({"out": m(x)["out"]}, t)
     (loss * scale).backward()
     assert abs(loss.item() - ref_loss.item()) <= 2 * abs(emu_loss.item() - ref_loss.item()) + 1e-4, \
@@ -343,4 +352,47 @@ def test_stf_cfg3_fullsize_train_fp16_gradients_vs_fp32():
     print(f"\nSTF cfg3 train fp16: loss {loss.item():.6f} vs {ref_loss.item():.6f} (emu {emu_loss.item():.6f}), "
           f"gradient rel median {errs[len(errs) // 2]:.3e}, tightest {worst[3]}: rel {worst[1]:.3e} "
           f"(emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
+    assert not bad, bad
+
+
+def test_unet_cfg2_fullsize_train_fp16_vs_fp32():
+    """configs[1] in the reference's --amp numerics (fp16 storage, GradScaler's 65536 loss
+    scale): logits, loss and every parameter gradient against the fp32 restatement, within
+    the fp16-storage emulation's band (the bf16 test's rule: err <= 2 err_emu + 0.03)."""
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    model, sd = _unet(seed=3)
+    model.storage_dtype = torch.float16
+    x, t = dce_batch(64, 8, 256, 256, seed=14, device=DEV)
+    x = x.flatten(1, 2)
+    p, ref_out, ref_loss = _oracle_train(sd, x, t, o_unet.forward)
+    scale = 65536.0
+    with o_unet_bf16.storage(torch.float16):
+        pe, emu_out, emu_loss = _oracle_train(sd, x, t, o_unet_bf16.forward, scale)
+    model.train()
+    out = model(x)["out"]
+    loss = criterion({"out": out}, t)
+    (loss * scale).backward()
+    e_out, e_emu_out = rel(out, ref_out), rel(emu_out, ref_out)
+    assert e_out <= 2 * e_emu_out + 2e-3, (e_out, e_emu_out)
+    assert abs(loss.item() - ref_loss) <= 2 * abs(emu_loss - ref_loss) + 1e-4, (loss.item(), ref_loss, emu_loss)
+    named = dict(model.named_parameters())
+    bad, worst = [], (-1.0, 0.0, 0.0, "")
+    for k, v in p.items():
+        if v.grad is None:
+            continue
+        got = named[k].grad / scale
+        if _bn_fed_bias(k):     # exact gradient 0 (a BatchNorm follows): absolute check
+            bound = v.grad.abs().max().item() + p[k.replace("bias", "weight")].grad.abs().mean().item()
+            if got.abs().max().item() > 0.05 * bound + 1e-5:
+                bad.append((k, "bias", got.abs().max().item()))
+            continue
+        e_hip, e_emu = rel(got, v.grad), rel(pe[k].grad, v.grad)
+        if e_hip > 2 * e_emu + 0.03:
+            bad.append((k, e_hip, e_emu))
+        worst = max(worst, (e_hip / (2 * e_emu + 0.03), e_hip, e_emu, k))
+    errs = sorted(rel(named[k].grad / scale, v.grad) for k, v in p.items() if v.grad is not None and not _bn_fed_bias(k))
+    print(f"\nUNet cfg2 train fp16: logits rel {e_out:.3e} (emu {e_emu_out:.3e}), loss {loss.item():.6f} vs "
+          f"{ref_loss:.6f} (emu {emu_loss:.6f}), gradient rel median {errs[len(errs) // 2]:.3e} max {errs[-1]:.3e}, "
+          f"tightest {worst[3]}: rel {worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
     assert not bad, bad
