@@ -159,9 +159,6 @@ const char* stf_wgrad_kernel_name(const stf_wgrad_args* a);
  * scratch: they are reduced in place (fixed order) and left clobbered. */
 int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs,
                      float* out, stf_stream_t stream);
-/* stf_wgrad then stf_wgrad_reduce(a->ws, a->splits, ..., out): one call per weight
- * gradient (ABI v9). */
-int stf_wgrad_reduced(const stf_wgrad_args* a, float* out, stf_stream_t stream);
 
 /* Per-channel column sums of a bf16 NHWC tensor (bias gradients of ConvT /
  * 1x1 convs, src/unet.py:28-37).  partial: [ceil(M/256)][C] scratch. */
@@ -245,15 +242,6 @@ int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int y_cstride,
                      int C, int groups, const float* mask_scale, const float* mask_shift,
                      const float* coef, void* dy, int dy_cstride, float* bias_partial,
                      float* dbias, stf_stream_t stream);
-/* stf_bn_bwd_finalize followed by stf_bn_bwd_apply on the same stream (coef written by
- * the first, read by the second), with both argument sets validated before either
- * launches: one call per training-mode BatchNorm backward (ABI v9). */
-int stf_bn_backward(float* partial, int tiles, const float* gamma, const float* mean,
-                    const float* invstd, float* dgamma, float* dbeta, float* coef,
-                    const void* g, int g_cstride, const void* y, int y_cstride, int64_t M,
-                    int C, int groups, const float* mask_scale, const float* mask_shift,
-                    void* dy, int dy_cstride, float* bias_partial, float* dbias,
-                    stf_stream_t stream);
 
 /* ---------------------------------------------------------------- head + loss
  * UNet OutConv fused with the last BN+ReLU (src/unet.py:16-17,37,56):

@@ -657,18 +657,3 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
   }
   return 0;
 }
-
-// finalize + apply in one call (one C-ABI crossing instead of two on the host-bound STF
-// step); every argument is validated before the first launch
-extern "C" int stf_bn_backward(float* partial, int tiles, const float* gamma, const float* mean, const float* invstd,
-                               float* dgamma, float* dbeta, float* coef, const void* g, int g_cstride, const void* y,
-                               int y_cstride, int64_t M, int C, int groups, const float* mask_scale,
-                               const float* mask_shift, void* dy, int dy_cstride, float* bias_partial, float* dbias,
-                               stf_stream_t stream) {
-  if (!cg_ok(C) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8 || groups < 1 || M % groups) return STF_EINVAL;
-  if ((mask_scale == nullptr) != (mask_shift == nullptr)) return STF_EINVAL;
-  const int rc = stf_bn_bwd_finalize(partial, tiles, groups, C, M, gamma, mean, invstd, dgamma, dbeta, coef, stream);
-  if (rc) return rc;
-  return stf_bn_bwd_apply(g, g_cstride, y, y_cstride, M, C, groups, mask_scale, mask_shift, coef, dy, dy_cstride,
-                          bias_partial, dbias, stream);
-}

@@ -786,12 +786,3 @@ extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, i
   STF_CHECK_LAUNCH();
   return 0;
 }
-
-// the weight gradient and its split reduction in one call (one C-ABI crossing)
-extern "C" int stf_wgrad_reduced(const stf_wgrad_args* a, float* out, stf_stream_t stream) {
-  const long total = (long)a->Nout * a->g.R * a->g.S * a->g.Cs;
-  if (!out || !a->ws || total % 8 || ((uintptr_t)a->ws & 15)) return STF_EINVAL;
-  const int rc = stf_wgrad(a, stream);
-  if (rc) return rc;
-  return stf_wgrad_reduce(a->ws, a->splits, a->Nout, a->g.R, a->g.S, a->g.Cs, out, stream);
-}

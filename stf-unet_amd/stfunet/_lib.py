@@ -67,7 +67,6 @@ _SIGS = {
     "stf_wgrad_plan": (c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_size_t)]),
     "stf_wgrad": (c_int, [ctypes.POINTER(WgradArgs), P]),
     "stf_wgrad_reduce": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
-    "stf_wgrad_reduced": (c_int, [ctypes.POINTER(WgradArgs), P, P]),
     "stf_channel_sum": (c_int, [P, c_int, c_int, c_int, P, P, P]),
     "stf_bn_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, c_float, c_float, P, P, P, P, P, P, P]),
     "stf_bn_running_batch": (c_int, [P, c_int, P]),
@@ -80,8 +79,6 @@ _SIGS = {
     "stf_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, P, P, P, P, P]),
     "stf_bn_bwd_apply_tiles": (c_int, [c_int64, c_int]),
     "stf_bn_bwd_apply": (c_int, [P, c_int, P, c_int, c_int64, c_int, c_int, P, P, P, P, c_int, P, P, P]),
-    "stf_bn_backward": (c_int, [P, c_int, P, P, P, P, P, P, P, c_int, P, c_int, c_int64, c_int, c_int, P, P, P, c_int,
-                                P, P, P]),
     "stf_head_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "stf_head_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P, P, P]),
     "stf_head_tiles": (c_int, [c_int, c_int, c_int, c_int]),

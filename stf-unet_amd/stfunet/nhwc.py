@@ -481,12 +481,10 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
         name = _kernel_name("stf_wgrad_kernel_name", ("w", x.N, x.H, x.W, x.C, dy.H, dy.W, dy.C, R, S, stride, pad), a)
         if not t.wants(name):
             t = None
-    if t is None:            # kernel + split reduction in one C-ABI call
-        call("stf_wgrad_reduced", ctypes.byref(a), out.data_ptr(), stream())
-        return
-    ev = t.begin()           # timed: the events bracket the weight-gradient kernel alone
+    ev = t.begin() if t is not None else None
     call("stf_wgrad", ctypes.byref(a), stream())
-    t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
+    if t is not None:
+        t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad_reduce", ws.data_ptr(), splits, dy.C, R, S, x.C, out.data_ptr(), stream())
 
 
@@ -678,17 +676,6 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                         dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
         dgamma = dbeta = None
-    if st.training:          # finalize + apply in one C-ABI call (dbias is None here)
-        dst = out if out is not None else g
-        if out is not None:
-            out.check()
-            assert (out.N, out.H, out.W, out.C) == (y.N, y.H, y.W, C)
-        if mask_relu:
-            assert out is not None
-        call("stf_bn_backward", _p(part), tiles, bn.weight.data_ptr(), _p(st.mean), _p(st.invstd), _p(dgamma),
-             _p(dbeta), _p(coef), g.ptr(), g.cs, y.ptr(), y.cs, y.M, C, G, _p(st.scale) if mask_relu else None,
-             _p(st.shift) if mask_relu else None, dst.ptr(), dst.cs, None, None, stream())
-        return dst
     call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     if not st.training:
