@@ -25,7 +25,8 @@ import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(HERE, "stf-unet_amd"))
+# STF_PKG_ROOT: import the package from another tree (same-box A/B of host-side changes)
+sys.path.insert(0, os.environ.get("STF_PKG_ROOT", os.path.join(HERE, "stf-unet_amd")))
 sys.path.insert(0, HERE)
 
 import torch  # noqa: E402
