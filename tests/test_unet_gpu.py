@@ -384,7 +384,26 @@ def test_gradscaler_step_on_device_and_inf_skip():
         assert torch.equal(v.grad, scaled[k]), k                 # still scaled, as with fused AdamW
         assert torch.allclose(v.detach(), ref[k].detach(), rtol=0, atol=1e-6), k
     assert int(opt.state_dict()["state"][0]["step"]) == 1
-    # 3) a plain (unscaled) step afterwards continues the count on the host path
+    # 3) unscale_ by the caller first (e.g. for gradient clipping): the scaler hands over no
+    #    scale, only the inf flag; the update equals torch's on the unscaled gradients
+    backward()
+    scaler.unscale_(opt)
+    unscaled = {k: v.grad.clone() for k, v in named.items()}
+    ref = {k: v.detach().clone().requires_grad_() for k, v in named.items()}
+    ref_opt = torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=1e-4, foreach=False)
+    ref_opt.load_state_dict({"state": {i: {kk: (vv.clone() if torch.is_tensor(vv) else vv)
+                                           for kk, vv in st.items()}
+                                       for i, st in opt.state_dict()["state"].items()},
+                             "param_groups": ref_opt.state_dict()["param_groups"]})
+    for k in ref:
+        ref[k].grad = unscaled[k]
+    scaler.step(opt)
+    scaler.update()
+    ref_opt.step()
+    for k, v in named.items():
+        assert torch.allclose(v.detach(), ref[k].detach(), rtol=0, atol=1e-6), k
+    assert int(opt.state_dict()["state"][0]["step"]) == 2
+    # 4) a plain (unscaled) step afterwards continues the count on the host path
     backward()
     opt.step()
-    assert int(opt.state_dict()["state"][0]["step"]) == 2
+    assert int(opt.state_dict()["state"][0]["step"]) == 3
