@@ -312,20 +312,25 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
   // 32-bit index math (a 64-bit division is a long emulated sequence per unit): every
   // tensor here has < 2^31 windows and pixels (checked by the host)
   const int HpWp = Hp * Wp, cshift = __builtin_ctz(CG);   // CG is a power of two (64 % CG == 0)
-  for (long u = gt; u < U; u += (long)tpg * PNT) {
-    const int win = (int)(u >> (2 + cshift)) + (int)(g * wpg);
+  // two units per iteration, all six loads issued before either is used (more bytes in
+  // flight per lane); the pair test is quad-uniform (U and the stride are multiples of 4)
+  const long S = (long)tpg * PNT;
+  auto pix = [&](long u, int& win) {
+    win = (int)(u >> (2 + cshift)) + (int)(g * wpg);
     const int n = win / HpWp;
     const int rem = win - n * HpWp;
     const int py = rem / Wp, px = rem - py * Wp;
-    const long p = ((long)(n * H + 2 * py + (d >> 1))) * W + 2 * px + (d & 1);
+    return ((long)(n * H + 2 * py + (d >> 1))) * W + 2 * px + (d & 1);
+  };
+  auto unit = [&](long p, int win, const uint4& yv, const uint4& zv, const uint4& pv) {
     float v[8], gd[8], dp[8];
-    unpack8(*reinterpret_cast<const uint4*>(y + p * ycs + cg * 8), v);
-    if (dz) unpack8(*reinterpret_cast<const uint4*>(dz + p * dzcs + cg * 8), gd);
+    unpack8(yv, v);
+    if (dz) unpack8(zv, gd);
     else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) gd[j] = 0.f;
     }
-    unpack8(*reinterpret_cast<const uint4*>(dpool + (long)win * C + cg * 8), dp);
+    unpack8(pv, dp);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float t = v[j] * sc[j] + sh[j];
@@ -342,6 +347,24 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
       sgx[j] += gj * (v[j] - mu[j]) * is[j];
     }
     *reinterpret_cast<uint4*>(g_out + p * C + cg * 8) = pack8(gd);
+  };
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+  for (long u = gt; u < U; u += 2 * S) {
+    const bool two = u + S < U;
+    int w0, w1 = 0;
+    const long p0 = pix(u, w0);
+    const long p1 = two ? pix(u + S, w1) : p0;
+    const uint4 y0 = *reinterpret_cast<const uint4*>(y + p0 * ycs + cg * 8);
+    const uint4 z0 = dz ? *reinterpret_cast<const uint4*>(dz + p0 * dzcs + cg * 8) : zero4;
+    const uint4 q0 = *reinterpret_cast<const uint4*>(dpool + (long)w0 * C + cg * 8);
+    uint4 y1 = zero4, z1 = zero4, q1 = zero4;
+    if (two) {
+      y1 = *reinterpret_cast<const uint4*>(y + p1 * ycs + cg * 8);
+      if (dz) z1 = *reinterpret_cast<const uint4*>(dz + p1 * dzcs + cg * 8);
+      q1 = *reinterpret_cast<const uint4*>(dpool + (long)w1 * C + cg * 8);
+    }
+    unit(p0, w0, y0, z0, q0);
+    if (two) unit(p1, w1, y1, z1, q1);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
