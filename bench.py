@@ -244,8 +244,37 @@ def cpu_baseline(args):
                       f"{args.cpu_steps} timed steps after 1 warm-up, {dt:.3f} s/step"}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD process -- nothing here has touched the GPU yet --
+    and return its exit code.  With a launcher (WORLD_SIZE set) --gpus must agree."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

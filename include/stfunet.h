@@ -395,6 +395,14 @@ int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int H, int W, i
  * int64 device arrays that ACCUMULATE (zero them first).  K <= 16. */
 int stf_eval_counts(const float* logits, const int64_t* target, int B, int K, int64_t HW,
                     int64_t ignore_index, int64_t* confmat, int64_t* dice_counts, stf_stream_t stream);
+/* The same pass with the Dice prediction taken from probs (same layout): the first argmax
+ * of torch.softmax(logits, 1), which is what DiceCoefficient.update argmaxes
+ * (train_and_eval.py:84-85) -- fp32 softmax can round logits that differ by less than an
+ * ulp of exp() into a tie that argmax(logits) would not see.  The confusion matrix keeps
+ * the logits' argmax (evaluate(), :331).  ABI v9. */
+int stf_eval_counts_sm(const float* logits, const float* probs, const int64_t* target, int B, int K,
+                       int64_t HW, int64_t ignore_index, int64_t* confmat, int64_t* dice_counts,
+                       stf_stream_t stream);
 
 /* ---------------------------------------------------------------- PK maps (extended Tofts)
  * pk_fitting.py ToftsModelFitter, all fp32.  The host builds

@@ -20,7 +20,7 @@ def confusion_matrix(target, pred, n):
 
 
 def dice_per_class(logits, target, num_classes=2, ignore_index=None):
-    pred = torch.argmax(logits, dim=1)
+    pred = torch.argmax(torch.softmax(logits, dim=1), dim=1)      # :84-85
     if ignore_index is not None:
         keep = (target != ignore_index)
         pred = pred * keep

@@ -388,7 +388,7 @@ extern "C" int stf_lstm_seq_fwd(const void* wcat, const float* bias, void* lbuf,
                                 void* h_last, int h_cstride, stf_stream_t stream) {
   if (P <= 0 || T <= 0) return 0;
   if (C != 64 || !wcat || !bias || !lbuf || !c_out || !h_last || h_cstride < C) return STF_EINVAL;
-  if (((uintptr_t)wcat & 15) || ((uintptr_t)lbuf & 15)) return STF_EINVAL;
+  if (((uintptr_t)wcat & 15) || ((uintptr_t)lbuf & 15) || ((uintptr_t)c_out & 15)) return STF_EINVAL;
   const dim3 grid((P + BM - 1) / BM);
   static const int occ = [] { const char* e = getenv("STF_LSTM_OCC"); return e ? atoi(e) : 2; }();
   if (occ == 1)

@@ -18,9 +18,11 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libstfunet_hip.so")
-# A/B measurements: STF_LIB points at another build of the same library (tools/ab_lib.sh)
+# A/B measurements: STF_LIB / STF_LIB_F16 point at other builds of the same libraries
+# (tools/ab_lib.sh); STF_LIB alone also moves the fp16 build to its directory
 LIB_PATH = os.environ.get("STF_LIB", LIB_PATH)
-LIB_PATHS = {torch.bfloat16: LIB_PATH, torch.float16: os.path.join(_HERE, "libstfunet_hip_f16.so")}
+LIB_PATH_F16 = os.environ.get("STF_LIB_F16", os.path.join(os.path.dirname(LIB_PATH), "libstfunet_hip_f16.so"))
+LIB_PATHS = {torch.bfloat16: LIB_PATH, torch.float16: LIB_PATH_F16}
 STORAGE_CODE = {torch.bfloat16: 0, torch.float16: 1}     # stf_storage_type()
 
 c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
@@ -98,6 +100,7 @@ _SIGS = {
     "stf_pack_weights_tiled": (c_int, [P, c_int, c_int, P]),
     "stf_pack_sequence": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_eval_counts": (c_int, [P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
+    "stf_eval_counts_sm": (c_int, [P, P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_tofts_forward": (c_int, [P, P, P, c_int, c_int, P, P, P, P, P, c_int, c_float, P, P]),
     "stf_tofts_fit": (c_int, [P, c_int, c_int, P, P, P, P, P, c_int, c_float, c_int, c_int, P, c_float, c_float,
                               c_float, P, P, P]),

@@ -14,8 +14,14 @@ Restates ``train_utils/train_and_eval.py`` (and re-exports the criterion of
 * ``train_one_epoch``       :377-411 (autocast when a GradScaler is given,
   zero_grad -> backward -> step -> per-iteration LR step -> ``loss.item()``)
 * ``create_lr_scheduler``   :414-438
+
+and the per-epoch artefacts of ``train.py``'s loop: ``results_file_name`` /
+``write_epoch_results`` (train.py:155-162, 289-301), ``print_eval`` (:278-284),
+``checkpoint_dict`` (:304-311, ``scaler`` key under ``--amp``), ``resume_from``
+(:249-256) and ``EarlyStopping`` (train_utils/early_stopping.py:9-24).
 """
 import datetime
+import os
 import time
 from collections import defaultdict, deque
 
@@ -90,7 +96,10 @@ class DiceCoefficient:
     def update(self, pred, target):
         if isinstance(pred, dict):
             pred = pred["out"]
-        pred = torch.argmax(pred, dim=1)          # argmax(softmax(x)) == argmax(x)
+        # softmax first, as the reference does (:84-85): fp32 softmax can round two logits that
+        # differ by less than an ulp of exp() to the same probability, and argmax then takes the
+        # first of the tie where argmax(x) would not
+        pred = torch.argmax(torch.softmax(pred, dim=1), dim=1)
         if self.ignore_index is not None:
             keep = target != self.ignore_index
             pred = pred * keep
@@ -240,10 +249,12 @@ class MetricLogger:
 
 
 def eval_update(out, target, confmat, dice):
-    """One batch of evaluate(): ``confmat.update(target, argmax)`` + ``dice.update(out,
-    target)`` as ONE stf_eval_counts pass over the logits (argmax, confusion counts,
-    per-class Dice counts; no host synchronisation), then the per-batch Dice from the
-    counts exactly as DiceCoefficient.update computes it (train_and_eval.py:80-118)."""
+    """One batch of evaluate(): ``confmat.update(target, output.argmax(1))`` +
+    ``dice.update(output, target)`` as ONE stf_eval_counts_sm pass (confusion counts from
+    the logits' first argmax, per-class Dice counts from the first argmax of
+    ``torch.softmax(output, 1)`` -- the very op DiceCoefficient.update runs, :84-85, so
+    near-ties round the same way; no host synchronisation), then the per-batch Dice from
+    the counts exactly as DiceCoefficient.update computes it (train_and_eval.py:80-118)."""
     from ._lib import call, stream
     from .nhwc import _p
     if not out.is_cuda:
@@ -256,8 +267,9 @@ def eval_update(out, target, confmat, dice):
         confmat.mat = torch.zeros((K, K), dtype=torch.int64, device=out.device)
     counts = torch.zeros((K, 3), dtype=torch.int64, device=out.device)
     ign = dice.ignore_index if dice.ignore_index is not None else -1
-    call("stf_eval_counts", _p(out), _p(target), B, K, out[0, 0].numel(), ign, _p(confmat.mat), _p(counts),
-         stream())
+    probs = torch.softmax(out, dim=1)
+    call("stf_eval_counts_sm", _p(out), _p(probs), _p(target), B, K, out[0, 0].numel(), ign, _p(confmat.mat),
+         _p(counts), stream())
     inter, psum, tsum = counts.float().unbind(1)
     union = psum + tsum
     d = torch.where(union > 0, 2.0 * inter / union.clamp_min(1.0), torch.ones_like(union))
@@ -342,3 +354,92 @@ def create_lr_scheduler(optimizer, num_step: int, epochs: int, warmup=True, warm
     assert num_step > 0 and epochs > 0
     return torch.optim.lr_scheduler.LambdaLR(
         optimizer, lr_lambda=lr_lambda(num_step, epochs, warmup, warmup_epochs, warmup_factor))
+
+
+# ---------------------------------------------------------------- train.py's epoch artefacts
+def results_file_name(model_name, use_pk_maps=False, now=None, out_dir="./output"):
+    """``./output/{model}_results_{MMDD-HHMM}{_pk}.txt`` (train.py:151-162); creates the
+    directory like the reference."""
+    now = now or datetime.datetime.now()
+    os.makedirs(out_dir, exist_ok=True)
+    return os.path.join(out_dir, "{}_results_{}{}.txt".format(model_name, now.strftime("%m%d-%H%M"),
+                                                            "_pk" if use_pk_maps else ""))
+
+
+def epoch_results_text(epoch, mean_loss, lr, eval_metrics):
+    """The block train.py:289-301 appends to the results file after every epoch."""
+    mm = eval_metrics["mean_metrics"]
+    return (f"[epoch: {epoch}]\n"
+            f"train_loss: {mean_loss:.4f}\n"
+            f"lr: {lr:.6f}\n"
+            f"dice: {eval_metrics['dice']:.4f}\n"
+            f"global_acc: {eval_metrics['global_accuracy']:.4f}\n"
+            f"mean_iou: {mm['miou']:.4f}\n"
+            f"mean_precision: {mm['mprecision']:.4f}\n"
+            f"mean_recall: {mm['mrecall']:.4f}\n"
+            f"{eval_metrics['confusion_matrix']}\n\n")
+
+
+def write_epoch_results(results_file, epoch, mean_loss, lr, eval_metrics):
+    if results_file:
+        with open(results_file, "a") as f:
+            f.write(epoch_results_text(epoch, mean_loss, lr, eval_metrics))
+
+
+def print_eval(eval_metrics):
+    """The validation printout of train.py:278-284."""
+    mm = eval_metrics["mean_metrics"]
+    print(eval_metrics["confusion_matrix"])
+    print(f"Dice coefficient: {eval_metrics['dice']:.4f}")
+    print(f"Global accuracy: {eval_metrics['global_accuracy']:.4f}")
+    print(f"Mean IoU: {mm['miou']:.4f}")
+    print(f"Mean precision: {mm['mprecision']:.4f}")
+    print(f"Mean recall: {mm['mrecall']:.4f}")
+
+
+def checkpoint_dict(model, optimizer, lr_scheduler, epoch, args, scaler=None):
+    """train.py:304-311: {'model', 'optimizer', 'lr_scheduler', 'epoch', 'args'} plus
+    'scaler' when training with --amp (a GradScaler)."""
+    save = {"model": model.state_dict(), "optimizer": optimizer.state_dict(),
+            "lr_scheduler": lr_scheduler.state_dict(), "epoch": epoch, "args": args}
+    if scaler is not None:
+        save["scaler"] = scaler.state_dict()
+    return save
+
+
+def resume_from(checkpoint, model, optimizer, lr_scheduler, scaler=None):
+    """train.py:249-256: load model / optimizer / scheduler (and the GradScaler under
+    --amp) and return the next epoch."""
+    model.load_state_dict(checkpoint["model"])
+    optimizer.load_state_dict(checkpoint["optimizer"])
+    lr_scheduler.load_state_dict(checkpoint["lr_scheduler"])
+    if scaler is not None and "scaler" in checkpoint:
+        scaler.load_state_dict(checkpoint["scaler"])
+    return checkpoint["epoch"] + 1
+
+
+class EarlyStopping:
+    """train_utils/early_stopping.py:9-24 (patience on a higher-is-better metric)."""
+
+    def __init__(self, patience=10, verbose=False):
+        self.patience = patience
+        self.counter = 0
+        self.best_score = None
+        self.early_stop = False
+        self.verbose = verbose
+
+    def step(self, metric):
+        if self.best_score is None:
+            self.best_score = metric
+            return False
+        if metric <= self.best_score:
+            self.counter += 1
+            if self.verbose:
+                print(f"EarlyStopping: {self.counter}/{self.patience} no improvement.")
+            if self.counter >= self.patience:
+                self.early_stop = True
+                return True
+        else:
+            self.best_score = metric
+            self.counter = 0
+        return False

@@ -69,6 +69,8 @@ class AdamW(torch.optim.Optimizer):
         if fb is not None and fb["key"] == key and fb["pptr"][0] == params[0].data_ptr() and \
                 fb["pptr"][-1] == params[-1].data_ptr():
             return fb
+        if fb is not None:      # re-laying: the device step count (GradScaler steps) is the truth
+            self._sync_host_step(gi, fb)
         offs, off = [], 0
         for p in params:
             offs.append(off)

@@ -243,13 +243,31 @@ def gen_lr(tae, out):
     np.savez_compressed(os.path.join(out, "lr_table.npz"), lr=np.array(lrs), num_step=10, epochs=3)
 
 
+def gen_keys(unet_mod, stf_mod, out):
+    """state_dict key order and shapes of the reference modules (the drop-in contract,
+    SURVEY.md 8(b)): UNet (in 8 / 11) and STFLSTMUNet with and without PK maps."""
+    mods = {"unet_in8": unet_mod.UNet(in_channels=8, num_classes=2, base_c=64),
+            "unet_in11": unet_mod.UNet(in_channels=11, num_classes=2, base_c=64),
+            "stf_t8": stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8),
+            "stf_t8_pk": stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8, use_pk_maps=True)}
+    res = {k: [[n, list(v.shape)] for n, v in m.state_dict().items()] for k, m in mods.items()}
+    res["param_counts"] = {k: sum(p.numel() for p in m.parameters()) for k, m in mods.items()}
+    res["stf_input_format"] = getattr(mods["stf_t8"], "input_format", None)
+    with open(os.path.join(out, "state_dict_keys.json"), "w") as f:
+        json.dump(res, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default=None, choices=["keys"], help="regenerate one fixture only")
     a = ap.parse_args()
     torch.set_num_threads(8)
     unet_mod, stf_mod, tae, dcl = load_reference(a.ref)
+    gen_keys(unet_mod, stf_mod, a.out)
+    if a.only == "keys":
+        return
     summary = {}
     summary.update(gen_unet_small(unet_mod, tae, a.out))
     summary.update(gen_unet_full(unet_mod, tae, a.out))

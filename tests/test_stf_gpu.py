@@ -253,6 +253,43 @@ def test_stem_im2col_gemm(P):
     assert rel(dw.view(64, kpad)[:, :kreal].view(64, cin, 7, 7), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("P", [3, 1])
+def test_stem_pk_gather_path(P):
+    """The PK-map stem (src/stf_lstm_unet.py:105,172-177 with use_pk_maps: Cin = 1 + P):
+    stf_pack_sequence packs frame t and the P maps into 8 zero-padded channels, the 7x7/s2/p3
+    conv runs as an 8-channel tap-gather igemm, and its weight gradient as a 7x7/s2/p3 wgrad
+    on Cs = 8 (STFProgram's stem_gather path, the one cfg5 trains through).  Packed input
+    bit-exact; conv output and the real 1 + P weight-gradient columns vs F.conv2d autograd on
+    bf16-rounded operands (rel L2 <= 1e-2); the padded columns' gradient is exactly 0."""
+    from stfunet import nhwc
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
+    B, T, H, W = 2, 3, 40, 48
+    cin = 1 + P
+    torch.manual_seed(P)
+    x = torch.randn(B, T + P, 1, H, W, device=DEV)
+    xin = nhwc.new_feat(T * B, H, W, 8, DEV)
+    call("stf_pack_sequence", _p(x), B, T + P, 1, H, W, T, P, 8, xin.ptr(), stream())
+    frames = torch.cat([torch.cat([x[:, t], x[:, T:, 0]], 1) for t in range(T)], 0)     # [T*B, cin, H, W]
+    got = xin.dense()
+    assert torch.equal(got[:, :cin].float(), bfr(frames))
+    assert got[:, cin:].abs().max().item() == 0
+    w = torch.randn(64, cin, 7, 7, device=DEV) * 0.05
+    ho, wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = nhwc.new_feat(T * B, ho, wo, 64, DEV)
+    nhwc.igemm(xin, nhwc.pack_weight(w, 0, 8), 64, y, 7, 7, 2, 3)
+    yr = F.conv2d(bfr(frames), bfr(w), stride=2, padding=3)
+    assert rel(y.dense(), yr) < 1e-2
+    dy = bfr(torch.randn_like(yr))
+    tmp = torch.empty(64 * 8 * 49, device=DEV)
+    nhwc.wgrad(feat_from(dy), xin, 7, 7, 2, 3, tmp, defer=False)
+    wr = bfr(w).requires_grad_(True)
+    F.conv2d(bfr(frames), wr, stride=2, padding=3).backward(dy)
+    dw = tmp.view(64, 8, 7, 7)
+    assert rel(dw[:, :cin], wr.grad) < 1e-2
+    assert dw[:, cin:].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("pk", [False, True])
 def test_stf_model_vs_golden(pk):
     from oracle.init import canonical_state_dict

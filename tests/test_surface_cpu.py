@@ -49,7 +49,7 @@ def test_library_exports_every_header_symbol(dtype):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
     assert set(syms) == set(_lib.EXPORTED)
-    assert lib.stf_abi_version() == 8
+    assert lib.stf_abi_version() == 9
     assert lib.stf_storage_type() == _lib.STORAGE_CODE[dtype]
     assert b"invalid argument" in lib.stf_error_string(100001)
 
@@ -156,3 +156,76 @@ def test_size_queries_depend_only_on_the_cached_signature():
                 q += (sp.value, nb.value)
             res.add(q)
         assert len(res) == 1, (N, Hs, Cs, nout, res)
+
+
+def _ref_keys():
+    import json
+    with open(os.path.join(GOLDEN, "state_dict_keys.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("which", ["unet_in8", "unet_in11", "stf_t8", "stf_t8_pk"])
+def test_state_dict_keys_match_reference_modules(which):
+    """Key order and shapes equal the reference modules' (tests/golden/state_dict_keys.json,
+    written by make_golden.py from src/unet.py and src/stf_lstm_unet.py imported by path):
+    UNet 136 keys, STFLSTMUNet 296 keys, 304 with PK maps."""
+    from stfunet import STFLSTMUNet, UNet
+    ref = _ref_keys()
+    m = {"unet_in8": lambda: UNet(8, 2, 64), "unet_in11": lambda: UNet(11, 2, 64),
+         "stf_t8": lambda: STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8),
+         "stf_t8_pk": lambda: STFLSTMUNet(in_channels=1, num_classes=2, time_steps=8, use_pk_maps=True)}[which]()
+    got = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert got == ref[which]
+    assert len(got) == {"unet_in8": 136, "unet_in11": 136, "stf_t8": 296, "stf_t8_pk": 304}[which]
+    assert sum(p.numel() for p in m.parameters()) == ref["param_counts"][which]
+    if which.startswith("stf"):          # no input_format attribute: preprocess_input passes through
+        assert getattr(m, "input_format", "time_sequence") == "time_sequence"
+
+
+def test_stf_accepts_reference_state_dict_roundtrip():
+    """A reference-shaped STF checkpoint (keys / shapes from the fixture) loads strictly."""
+    from stfunet import STFLSTMUNet
+    ref = _ref_keys()["stf_t8_pk"]
+    sd = {k: torch.full(shape, 0.5) if shape else torch.tensor(3) for k, shape in ref}
+    m = STFLSTMUNet(use_pk_maps=True)
+    m.load_state_dict(sd, strict=True)
+    assert torch.equal(m.state_dict()["lstm4.weight_hh_l0"], torch.full((2048, 512), 0.5))
+
+
+def test_epoch_results_file_and_checkpoint_dict(tmp_path):
+    """train.py:151-162 results-file name, the per-epoch block of :289-301, the checkpoint
+    dict of :304-311 (+ 'scaler' under --amp), resume_from (:249-256) and EarlyStopping
+    (early_stopping.py:9-24)."""
+    import datetime
+    from stfunet import engine
+    from stfunet.unet import UNet
+    now = datetime.datetime(2025, 5, 23, 9, 7)
+    path = engine.results_file_name("stflstm", use_pk_maps=True, now=now, out_dir=str(tmp_path / "output"))
+    assert path == str(tmp_path / "output" / "stflstm_results_0523-0907_pk.txt")
+    assert engine.results_file_name("unet", now=now, out_dir=str(tmp_path)).endswith("unet_results_0523-0907.txt")
+    cm = engine.ConfusionMatrix(2)
+    cm.update(torch.tensor([0, 0, 1, 1, 1]), torch.tensor([0, 1, 1, 1, 0]))
+    em = {"dice": 0.61234, "global_accuracy": 0.6, "confusion_matrix": cm,
+          "mean_metrics": {"miou": 0.41666, "mprecision": 0.58333, "mrecall": 0.58333}}
+    engine.write_epoch_results(path, 3, 0.123456, 1e-3 / 3, em)
+    engine.write_epoch_results(path, 4, 0.1, 2e-4, em)
+    text = open(path).read()
+    block = ("[epoch: 3]\ntrain_loss: 0.1235\nlr: 0.000333\ndice: 0.6123\nglobal_acc: 0.6000\n"
+             "mean_iou: 0.4167\nmean_precision: 0.5833\nmean_recall: 0.5833\n"
+             "global correct: 60.0\naverage row correct: ['50.0', '66.7']\nIoU: ['33.3', '50.0']\n"
+             "mean IoU: 41.7\n\n")
+    assert text.startswith(block) and text.count("[epoch: ") == 2
+    m = UNet(8, 2, 8)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    sch = engine.create_lr_scheduler(opt, 4, 3)
+    scaler = torch.amp.GradScaler("cuda", enabled=False)
+    ck = engine.checkpoint_dict(m, opt, sch, 5, {"amp": False})
+    assert set(ck) == {"model", "optimizer", "lr_scheduler", "epoch", "args"}
+    ck = engine.checkpoint_dict(m, opt, sch, 5, {"amp": True}, scaler=scaler)
+    assert set(ck) == {"model", "optimizer", "lr_scheduler", "epoch", "args", "scaler"}
+    m2 = UNet(8, 2, 8)
+    opt2 = torch.optim.AdamW(m2.parameters(), lr=1e-3)
+    assert engine.resume_from(ck, m2, opt2, engine.create_lr_scheduler(opt2, 4, 3), scaler) == 6
+    assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m2.state_dict().values()))
+    es = engine.EarlyStopping(patience=2)
+    assert [es.step(v) for v in (0.5, 0.6, 0.6, 0.55)] == [False, False, False, True] and es.early_stop

@@ -238,6 +238,49 @@ def test_checkpoint_resume_bitwise():
     assert sched2.get_last_lr() == sched.get_last_lr()
 
 
+def test_checkpoint_resume_bitwise_amp_scaler():
+    """--amp variant of the resume contract: train_one_epoch with a GradScaler (autocast
+    fp16, train_and_eval.py:389-404), checkpoint through engine.checkpoint_dict (train.py:
+    304-311, which adds the 'scaler' key under --amp) and torch.save/load(weights_only=True),
+    then engine.resume_from into a FRESH model, AdamW, LambdaLR and GradScaler (train.py:
+    249-256): the next epoch matches the uninterrupted run bit for bit, the scaler's scale and
+    growth tracker included.  A growth_interval of 2 makes the scale change inside the run."""
+    import io
+    from stfunet import engine
+    from stfunet.optim import AdamW
+    batches = [dce_case(51 + i, 2, 8, 64, 64) for i in range(6)]
+
+    def make(seed):
+        model, _ = _model(8, seed=seed)
+        opt = AdamW(list(model.parameters()), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
+        scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 14, growth_interval=2)
+        return model, opt, engine.create_lr_scheduler(opt, 3, 3, warmup=True), scaler
+
+    model, opt, sched, scaler = make(9)
+    dev = torch.device(DEV)
+    engine.train_one_epoch(model, opt, batches[:3], dev, 0, 2, lr_scheduler=sched, print_freq=100, scaler=scaler)
+    ck = engine.checkpoint_dict(model, opt, sched, 0, {"lr": 1e-3, "epochs": 3, "amp": True}, scaler=scaler)
+    assert set(ck) == {"model", "optimizer", "lr_scheduler", "epoch", "args", "scaler"}
+    buf = io.BytesIO()
+    torch.save(ck, buf)
+    engine.train_one_epoch(model, opt, batches[3:], dev, 1, 2, lr_scheduler=sched, print_freq=100, scaler=scaler)
+    want = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    want_scaler = scaler.state_dict()
+
+    buf.seek(0)
+    ck = torch.load(buf, weights_only=True, map_location=DEV)
+    model2, opt2, sched2, scaler2 = make(123)
+    start = engine.resume_from(ck, model2, opt2, sched2, scaler2)
+    assert start == 1 and scaler2.get_scale() == ck["scaler"]["scale"]
+    engine.train_one_epoch(model2, opt2, batches[3:], dev, start, 2, lr_scheduler=sched2, print_freq=100,
+                           scaler=scaler2)
+    got = model2.state_dict()
+    for k, v in want.items():
+        assert torch.equal(got[k], v), k
+    assert scaler2.state_dict() == want_scaler
+    assert sched2.get_last_lr() == sched.get_last_lr()
+
+
 def test_unet_eval_mode_backward_vs_oracle():
     """Backward through eval-mode BatchNorm (running statistics are constants: dy = gamma *
     invstd * g, conv biases get sum(dy) != 0) vs autograd of the fp32 oracle in eval mode;
