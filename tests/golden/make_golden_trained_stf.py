@@ -1,0 +1,104 @@
+"""STF trained-Dice fixture, produced by running the REFERENCE training code (build container only).
+
+    python tests/golden/make_golden_trained_stf.py  [--ref /root/reference]
+
+The STF twin of ``make_golden_trained.py``.  ``src/stf_lstm_unet.py`` ``STFLSTMUNet(in_channels=1,
+num_classes=2, time_steps=4)`` (imported by path with the standard BasicBlock ResNet-34 stand-in
+for the absent torchvision, as in ``make_golden.py``) from ``oracle.init``'s canonical weights (seed 0)
+is trained by the reference's own ``train_one_epoch`` (``train_and_eval.py:377-411``: CE + Dice,
+``torch.optim.AdamW(fused=True)`` with ``train.py:230-237``'s hyper-parameters, the per-iteration
+``create_lr_scheduler``) for ``EPOCHS`` x ``STEPS`` steps of ``dce_case`` batches ([B=4, T=4, 1, 64,
+64], seeds 3000+, half-resolution 32^2 targets: the reference predicts at H/2, SURVEY.md section 0
+defect 1), then scored by its own ``evaluate`` (``train_and_eval.py:316-374``) on ``EVAL_BATCHES``
+held-out batches (seeds 4000+).
+
+ResNet-34's 27 M parameters (55 MB even in 16 bits) are not committed: the fixture holds the Dice,
+the confusion matrix, the per-pixel argmax, the training losses -- and the Dice of a SECOND
+reference run that differs only in the CPU thread count (reduction order), the reference's own
+run-to-run spread, which sets the tolerance of the gfx950 training test.
+
+Output: ``tests/golden/stf_trained.npz`` (no pickles).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+from make_golden import load_reference  # noqa: E402
+from oracle.cases import dce_case  # noqa: E402
+from oracle.init import canonical_state_dict  # noqa: E402
+
+B, T, HW = 4, 4, 64
+EPOCHS, STEPS = 8, 40
+EVAL_BATCHES = 4
+
+
+def train_batches(epoch):
+    return [dce_case(3000 + epoch * STEPS + i, B, T, HW, HW, target_hw=(HW // 2, HW // 2)) for i in range(STEPS)]
+
+
+def eval_batches():
+    return [dce_case(4000 + i, B, T, HW, HW, target_hw=(HW // 2, HW // 2)) for i in range(EVAL_BATCHES)]
+
+
+def train_and_eval(stf_mod, tae, threads):
+    torch.set_num_threads(threads)
+    model = stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
+    model.load_state_dict(canonical_state_dict(model.state_dict(), seed=0))
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3,
+                            betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8, fused=True)
+    sched = tae.create_lr_scheduler(opt, STEPS, EPOCHS, warmup=True)
+    losses = []
+    for ep in range(EPOCHS):
+        mean_loss, lr = tae.train_one_epoch(model, opt, train_batches(ep), torch.device("cpu"), ep, 2,
+                                            lr_scheduler=sched, print_freq=1000)
+        losses.append(mean_loss)
+        print(f"[{threads} threads] epoch {ep}: mean loss {mean_loss:.4f} lr {lr:.2e}", flush=True)
+    ev = eval_batches()
+    metrics = tae.evaluate(model, ev, torch.device("cpu"), num_classes=2)
+    model.eval()
+    preds, margins = [], []
+    with torch.no_grad():
+        for x5, _ in ev:
+            lo = model(tae.preprocess_input(x5, model))["out"]
+            preds.append(lo.argmax(1).numpy().astype(np.uint8))
+            margins.append((lo[:, 1] - lo[:, 0]).abs().numpy().astype(np.float32))
+    return metrics, np.concatenate(preds), np.concatenate(margins), losses
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=HERE)
+    a = ap.parse_args()
+    _, stf_mod, tae, _ = load_reference(a.ref)
+    metrics, pred, margin, losses = train_and_eval(stf_mod, tae, 8)
+    metrics2, pred2, _, _ = train_and_eval(stf_mod, tae, 3)
+    res = dict(
+        dice=np.array(metrics["dice"]),
+        dice_other_threads=np.array(metrics2["dice"]),
+        confmat=metrics["confusion_matrix"].mat.numpy(),
+        pred_bits=np.packbits(pred.reshape(-1)),
+        pred_shape=np.array(pred.shape),
+        margin=margin.astype(np.float16),
+        train_losses=np.array(losses),
+        config=np.array([B, T, HW, EPOCHS, STEPS, EVAL_BATCHES]),
+    )
+    np.savez_compressed(os.path.join(a.out, "stf_trained.npz"), **res)
+    print(json.dumps({"dice": metrics["dice"], "dice_3_threads": metrics2["dice"],
+                      "confmat": metrics["confusion_matrix"].mat.tolist(),
+                      "pred_flips_between_thread_counts": int((pred != pred2).sum()),
+                      "margin_lt_1e-1": int((margin < 1e-1).sum()), "pixels": int(margin.size),
+                      "losses": losses}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

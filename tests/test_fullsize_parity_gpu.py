@@ -12,6 +12,10 @@ with every stored activation rounded to bf16) runs beside it to set the rounding
                     scores with Dice) flipped vs fp32 on at most 2 * flips_emu + 1e-4 of the
                     4.2 M pixels, and |Dice_hip - Dice_fp32| <= 2 * |Dice_emu - Dice_fp32| + 1e-4
   STF eval mode     logits rel-L2 <= 2 * err_emu + 2e-3 (as test_stf_eval_mode_vs_oracle)
+  STF train mode    logits rel-L2 <= 1.3 * err_emu + 0.01 and <= 1.3 * err of the reference's own
+                    torch.autocast(bf16) step (the restatement under autocast, same GPU), every
+                    parameter gradient <= 2 * err_emu + 0.03 (bf16 at T = 8 / 16; fp16 + GradScaler
+                    at cfg3 and at cfg5's 512^2, T = 32 + PK)
 """
 import pytest
 import torch
@@ -195,12 +199,31 @@ def test_unet_cfg2_fullsize_eval_fp16_storage_vs_fp32():
     assert e_hip <= 2 * e_emu + 2e-4, (e_hip, e_emu)
 
 
+def _grad_band(m, p, pe, scale=1.0, slack=0.03):
+    """Every parameter gradient of the HIP model within 2 x the 16-bit emulation's error +
+    ``slack`` of the fp32 restatement's; returns (violations, tightest, sorted errors)."""
+    bad, worst, errs = [], (-1.0, 0.0, 0.0, ""), []
+    for k, prm in m.named_parameters():
+        e_hip, e_emu = rel(prm.grad / scale, p[k].grad), rel(pe[k].grad, p[k].grad)
+        errs.append(e_hip)
+        if e_hip > 2 * e_emu + slack:
+            bad.append((k, e_hip, e_emu))
+        worst = max(worst, (e_hip / (2 * e_emu + slack), e_hip, e_emu, k))
+    return bad, worst, sorted(errs)
+
+
 @pytest.mark.parametrize("T", [8, 16])
 def test_stf_fullsize_train_vs_fp32(T):
-    """configs[2] (T=8) and configs[3]'s per-GPU workload (T=16), B=16, 256^2, train mode:
-    loss and logits within the bf16-emulation band (whole-model STF gradients are chaotic
-    under 16-bit storage at initialisation -- see tests/test_stf_gpu.py -- so they are only
-    checked finite here; the components carry the gradient parity)."""
+    """configs[2] (T=8) and configs[3]'s per-GPU workload (T=16), B=16, 256^2, bf16 storage,
+    TRAIN mode (batch statistics) against autograd of the fp32 restatement:
+      logits  rel-L2 <= 1.3 x the bf16 emulation's + 0.01 (round 2: 2x + 0.05);
+      loss    within 0.03;
+      every parameter gradient within 2 x the emulation's error + 0.03 (the UNet rule).
+    The band is wide because the model at initialisation is chaotic under ANY 16-bit rounding
+    in train mode: measured on the CPU restatement, rounding only the network
+    input to bf16 moves the logits by 5 % and the gradients by 55 % (median); keeping every
+    pre-BN conv output in fp32 still leaves 13 % / 76 % -- no storage layout removes it.  The
+    same amplification is what the reference's own bf16 autocast step shows (printed)."""
     import oracle.unet_bf16 as o_q
     from oracle import stf as o_stf, stf_bf16 as o_emu
     from stfunet import STFLSTMUNet
@@ -212,20 +235,82 @@ def test_stf_fullsize_train_vs_fp32(T):
     m = m.to(DEV).train()
     sd = {k: v.to(DEV) for k, v in sd.items()}
     x, t = dce_batch(16, T, 256, 256, seed=10 + T, device=DEV, mask_hw=(128, 128))
-    with torch.no_grad():
-        ref = o_stf.forward({k: v.clone() for k, v in sd.items()}, x, True)["out"]
-        with o_q.storage(torch.bfloat16):
-            emu = o_emu.forward({k: v.clone() for k, v in sd.items()}, x, True)["out"]
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref = o_stf.forward(p, x, True)["out"]
+    ref_loss = o_loss.criterion(ref, t)
+    ref_loss.backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.bfloat16):
+        emu = o_emu.forward(pe, x, True)["out"]
+        o_loss.criterion(emu, t).backward()
+    pa = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    try:                                                     # informational: the reference's own bf16 step
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            auto = o_stf.forward(pa, x, True)["out"].float()
+        o_loss.criterion(auto, t).backward()
+    except Exception as exc:                                 # noqa: BLE001
+        print(f"\nautocast-bf16 restatement unavailable: {exc!r}")
+        auto = None
     out = m(x)["out"]
     loss = criterion({"out": out}, t)
     loss.backward()
-    ref_loss = o_loss.criterion(ref, t).item()
     e_hip, e_emu = rel(out, ref), rel(emu, ref)
-    print(f"\nSTF T={T} train: logits rel {e_hip:.3e} (emu {e_emu:.3e}, hip vs emu {rel(out, emu):.3e}), loss {loss.item():.5f} vs {ref_loss:.5f}")
-    assert e_hip <= 2 * e_emu + 0.05, (e_hip, e_emu)
-    assert abs(loss.item() - ref_loss) < 0.03
-    for k, p in m.named_parameters():
-        assert p.grad is not None and torch.isfinite(p.grad).all(), k
+    e_auto = rel(auto, ref) if auto is not None else float("nan")
+    bad, worst, errs = _grad_band(m, p, pe)
+    ga = sorted(rel(pa[k].grad, p[k].grad) if pa[k].grad is not None else float("nan")
+                for k, _ in m.named_parameters())
+    print(f"\nSTF T={T} train bf16: logits rel {e_hip:.3e} (emu {e_emu:.3e}, reference autocast-bf16 {e_auto:.3e}, "
+          f"hip vs emu {rel(out, emu):.3e}), loss {loss.item():.5f} vs {ref_loss.item():.5f}; gradient rel median "
+          f"{errs[len(errs) // 2]:.3e} (autocast-bf16 {ga[len(ga) // 2]:.3e}), tightest {worst[3]}: "
+          f"{worst[1]:.3e} (emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
+    assert e_hip <= 1.3 * e_emu + 0.01, (e_hip, e_emu)
+    if auto is not None:     # no worse than the reference's own bf16 step (measured: 0.181 vs 0.185)
+        assert e_hip <= 1.3 * e_auto + 0.01, (e_hip, e_auto)
+        assert errs[len(errs) // 2] <= 1.2 * ga[len(ga) // 2] + 0.02, (errs[len(errs) // 2], ga[len(ga) // 2])
+    assert abs(loss.item() - ref_loss.item()) < 0.03
+    assert not bad, bad
+
+
+def test_stf_cfg5_fullsize_train_fp16_gradients_vs_fp32():
+    """configs[4]'s training step (512^2, T=32 DCE frames + 3 PK maps, fp16 storage + the
+    GradScaler-scaled loss of the reference's --amp step, TRAIN mode, B = 1 bounds the fp32
+    reference's memory): the PK stem (8-channel gather conv and its 7x7/s2 weight gradient),
+    PK fusion at every scale, the T=32 LSTMs and the decoder -- loss within 2x the fp16
+    emulation's error + 1e-4 and every parameter gradient within 2x the emulation's error +
+    0.03 of autograd of the fp32 restatement (the cfg3 fp16 rule)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf as o_stf, stf_bf16 as o_emu
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=32, use_pk_maps=True)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    m.storage_dtype = torch.float16
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = dce_batch(1, 32, 512, 512, seed=15, device=DEV, pk_channels=3, mask_hw=(256, 256))
+    scale = 65536.0
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref_loss = o_loss.criterion(o_stf.forward(p, x, True, use_pk_maps=True)["out"], t)
+    ref_loss.backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.float16):
+        emu_loss = o_loss.criterion(o_emu.forward(pe, x, True, use_pk_maps=True)["out"], t)
+        (emu_loss * scale).backward()
+    for v in pe.values():
+        if v.grad is not None:
+            v.grad.div_(scale)
+    loss = criterion({"out": m(x)["out"]}, t)
+    (loss * scale).backward()
+    bad, worst, errs = _grad_band(m, p, pe, scale)
+    print(f"\nSTF cfg5 train fp16: loss {loss.item():.6f} vs {ref_loss.item():.6f} (emu {emu_loss.item():.6f}), "
+          f"gradient rel median {errs[len(errs) // 2]:.3e}, tightest {worst[3]}: rel {worst[1]:.3e} "
+          f"(emu {worst[2]:.3e}, {worst[0]:.2f} of the band)")
+    assert abs(loss.item() - ref_loss.item()) <= 2 * abs(emu_loss.item() - ref_loss.item()) + 1e-4, \
+        (loss.item(), ref_loss.item(), emu_loss.item())
+    assert not bad, bad
+    assert m.conv1.weight.grad[:, 1:].abs().max() > 0           # the PK columns of the stem learn
 
 
 @pytest.mark.parametrize("T", [8, 16])
