@@ -198,6 +198,44 @@ def dice_vs_reference(dev, dtype):
                       f"[{b}, {t}, 1, {hw}, {hw}] (tests/golden/unet_trained.npz)"}
 
 
+def dice_vs_reference_stf(dev, dtype):
+    """STF "Dice vs ref": tests/golden/stf_trained.npz holds the Dice the reference's own
+    train_one_epoch + evaluate reached training STFLSTMUNet(T=4) from the canonical init on seeded
+    64^2 DCE stacks (make_golden_trained_stf.py; no weights: 27 M parameters), and of the same
+    reference run at another CPU thread count.  Here the same training runs on the gfx950 path
+    (engine.train_one_epoch, stfunet AdamW, same batches and schedule) and engine.evaluate scores
+    it on the same held-out batches; the fixture is data (seeds, the reference's Dice)."""
+    import contextlib
+    import numpy as np
+    from stfunet import STFLSTMUNet, engine
+    from stfunet.optim import AdamW
+    from stfunet.synthetic import canonical_state_dict, splitmix_dce_case
+    z = np.load(os.path.join(HERE, "tests", "golden", "stf_trained.npz"))
+    b, t, hw, epochs, steps, n_eval = (int(v) for v in z["config"])
+    tgt = (hw // 2, hw // 2)
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=t)
+    m.load_state_dict(canonical_state_dict(m.state_dict(), seed=0))
+    m.storage_dtype = torch.float16 if dtype == "fp16" else torch.bfloat16
+    m = m.to(dev)
+    opt = AdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4,
+                eps=1e-8)
+    sched = engine.create_lr_scheduler(opt, steps, epochs, warmup=True)
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(sys.stderr):
+        for ep in range(epochs):
+            batches = [splitmix_dce_case(3000 + ep * steps + i, b, t, hw, hw, target_hw=tgt) for i in range(steps)]
+            engine.train_one_epoch(m, opt, batches, dev, ep, 2, lr_scheduler=sched, print_freq=10 ** 6)
+        ev = [splitmix_dce_case(4000 + i, b, t, hw, hw, target_hw=tgt) for i in range(n_eval)]
+        got = engine.evaluate(m, ev, dev, num_classes=2)
+    ref = float(z["dice"])
+    return {"value": round(got["dice"], 6), "reference": round(ref, 6), "abs_diff": abs(got["dice"] - ref),
+            "reference_rerun_other_threads": round(float(z["dice_other_threads"]), 6), "tolerance": 5e-3,
+            "storage": dtype, "train_s": round(time.perf_counter() - t0, 2),
+            "sample": f"STFLSTMUNet(T={t}) trained {epochs}x{steps} steps from the canonical init on seeded "
+                      f"[{b}, {t}, 1, {hw}, {hw}] stacks, then evaluate() on {n_eval} held-out batches "
+                      f"(tests/golden/stf_trained.npz)"}
+
+
 def cpu_baseline(args):
     """fp32 oracle (plain PyTorch CPU restatement of src/unet.py or
     src/stf_lstm_unet.py + criterion + AdamW) on a bounded sample: B=2 at the
@@ -435,7 +473,8 @@ def main():
             "last_loss": round(last_loss, 5),
         }
         if not args.no_dice and world == 1:    # evaluate() all-reduces: rank 0 alone must not call it at N > 1
-            res["dice_vs_ref"] = dice_vs_reference(dev, args.dtype)
+            res["dice_vs_ref"] = (dice_vs_reference(dev, args.dtype) if args.model == "unet"
+                                  else dice_vs_reference_stf(dev, args.dtype))
         if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)

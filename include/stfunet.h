@@ -371,6 +371,19 @@ int stf_lstm_seq_supported(int C);
 int stf_lstm_seq_bwd(const void* wcat, const void* wcat_t, const float* bias, const void* lbuf, int P, int T,
                      int C, const float* c_all, const void* dh_last, int dh_cstride, void* dgates, void* dx,
                      int dx_cstride, stf_stream_t stream);
+/* Whole-sequence forward for C = 128 / 256 / 512 (stf_lstm_coop_supported) in ONE persistent
+ * launch: the 4C gate rows are cut into C/32 slices of 128; the C/32 workgroups of a 64-pixel
+ * block keep their weight slice in registers and hand h_t to each other through lbuf inside
+ * the launch (agent-scope counters, write-through stores, an acquire per step).  Same
+ * arguments, layout and values (bit for bit) as stf_lstm_seq_fwd / the per-step path, plus
+ * `sync`: a caller-owned device buffer of stf_lstm_coop_sync_bytes(P, T) bytes (16-B aligned;
+ * zeroed on the stream by the call itself; its last word is an error flag that
+ * stf_lstm_coop_error copies out: nonzero = a step's hand-off timed out).  ABI v9. */
+size_t stf_lstm_coop_sync_bytes(int P, int T);
+int stf_lstm_coop_supported(int C);
+int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
+                      void* h_last, int h_cstride, unsigned* sync, stf_stream_t stream);
+int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* out, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
 int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,
                          float* dw_hh, float* db_ih, float* db_hh, stf_stream_t stream);

@@ -593,7 +593,8 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
 // (16 split-lanes r x 16 column threads c) sums slabs r, r+16, ... of outputs
 // 4c..4c+3 with float4 loads (a wave reads 4 slabs x 256 contiguous bytes), the
 // 16 lane totals are added in fixed order, and the result is written in the
-// PyTorch [Nout][Cs][R][S] layout.
+// PyTorch [Nout][Cs][R][S] layout.  For plans with many splits (the high-resolution
+// layers: 32-512 slabs of a small output).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int Nout, int R,
                                                            int S, int Cs, float* __restrict__ out) {
   __shared__ double red[16][65];
@@ -629,6 +630,46 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
       out[((long)n * Cs + ch) * (R * S) + tap] = (float)t;
     }
   }
+}
+
+// Few-split plans (<= 8 slabs: the deep layers, whose slabs are a large output -- up to
+// 1024 x 1024 x 9 -- rather than many partials of a small one; the transposed store above would
+// scatter 4-B writes 36 B apart over tens of MB, 0.9-3.2 TB/s measured): a thread owns 4
+// consecutive (n, c) columns of ONE tap and sums its float4 over every slab (fixed order,
+// fp64, four slabs in flight); thread index = column-group * RS + tap, so a wave's scalar
+// stores out[(col + j) * RS + tap] fill a contiguous run of the [Nout][Cs][R][S] output
+// (tools/bench_wreduce.py: 2 x 1024 x 1024 x 9 slabs 82 -> 22 us, 4 x 1024 x 512 43 -> 18 us,
+// 8 x 512 x 512 23 -> 17 us; from 14 slabs up the kernel above is faster).
+template <int RS>
+__global__ __launch_bounds__(256) void wgrad_reduce_tap_kernel(const float* __restrict__ ws, int splits, int Nout,
+                                                               int Cs, float* __restrict__ out) {
+  const long cols = (long)Nout * Cs;
+  const long u = blockIdx.x * 256L + threadIdx.x;
+  const long cg = u / RS;
+  const int tap = (int)(u - cg * RS);
+  const long col = cg * 4;
+  if (col >= cols) return;
+  const long total = cols * RS;
+  const int n = (int)(col / Cs), ch = (int)(col - (long)n * Cs);
+  const float* p = ws + (long)n * RS * Cs + tap * Cs + ch;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int k = 0;
+  for (; k + 3 < splits; k += 4) {
+    const float4 u0 = *reinterpret_cast<const float4*>(p + (long)k * total);
+    const float4 u1 = *reinterpret_cast<const float4*>(p + (long)(k + 1) * total);
+    const float4 u2 = *reinterpret_cast<const float4*>(p + (long)(k + 2) * total);
+    const float4 u3 = *reinterpret_cast<const float4*>(p + (long)(k + 3) * total);
+    a0 += ((double)u0.x + u1.x) + ((double)u2.x + u3.x);
+    a1 += ((double)u0.y + u1.y) + ((double)u2.y + u3.y);
+    a2 += ((double)u0.z + u1.z) + ((double)u2.z + u3.z);
+    a3 += ((double)u0.w + u1.w) + ((double)u2.w + u3.w);
+  }
+  for (; k < splits; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(p + (long)k * total);
+    a0 += v.x; a1 += v.y; a2 += v.z; a3 += v.w;
+  }
+  float* o = out + col * RS + tap;
+  o[0] = (float)a0; o[RS] = (float)a1; o[2 * RS] = (float)a2; o[3 * RS] = (float)a3;
 }
 
 bool big_tile(const stf_wgrad_args* a) { return a->Nout % 128 == 0 && a->g.Cs % 128 == 0; }
@@ -781,8 +822,20 @@ extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, i
                                 stf_stream_t stream) {
   const long total = (long)Nout * R * S * Cs;
   if (total % 8 || ((uintptr_t)ws & 15)) return STF_EINVAL;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, (hipStream_t)stream, ws,
-                     splits, Nout, R, S, Cs, out);
+  hipStream_t s = (hipStream_t)stream;
+  const int rs = R * S;
+  static const int mode = [] { const char* e = getenv("STF_WRED_MODE"); return e ? atoi(e) : -1; }();
+  const bool shape_ok = (rs == 9 || rs == 4 || rs == 1) && ((long)Nout * Cs) % 4 == 0;
+  const int m = mode >= 0 ? mode : (shape_ok && splits <= 8) ? 2 : 0;
+  if (m == 2 && shape_ok) {
+    const unsigned blocks = (unsigned)(((long)Nout * Cs / 4 * rs + 255) / 256);
+    if (rs == 9) hipLaunchKernelGGL(wgrad_reduce_tap_kernel<9>, dim3(blocks), dim3(256), 0, s, ws, splits, Nout, Cs, out);
+    else if (rs == 4) hipLaunchKernelGGL(wgrad_reduce_tap_kernel<4>, dim3(blocks), dim3(256), 0, s, ws, splits, Nout, Cs, out);
+    else hipLaunchKernelGGL(wgrad_reduce_tap_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, splits, Nout, Cs, out);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, s, ws, splits, Nout, R,
+                       S, Cs, out);
+  }
   STF_CHECK_LAUNCH();
   return 0;
 }

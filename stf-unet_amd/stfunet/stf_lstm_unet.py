@@ -190,6 +190,22 @@ class LSTMProgram:
         return (os.environ.get("STF_LSTM_SEQ", "1") != "0" and bool(_lib.load().stf_lstm_seq_supported(self.C))
                 and lbuf.off == 0 and lbuf.cs == 2 * self.C and hT.cs >= self.C)
 
+    def coop(self, lbuf: Feat, hT: Feat):
+        """Cooperative whole-sequence forward (stf_lstm_coop_fwd, C = 128 / 256 / 512)?
+        STF_LSTM_COOP=0 keeps the per-step launches (A/B)."""
+        return (os.environ.get("STF_LSTM_COOP", "1") != "0" and bool(_lib.load().stf_lstm_coop_supported(self.C))
+                and lbuf.off == 0 and lbuf.cs == 2 * self.C and hT.cs >= self.C and hT.cs % 8 == 0
+                and hT.ptr() % 16 == 0)
+
+    def coop_error(self):
+        """Nonzero if the last cooperative forward's in-launch hand-off timed out (syncs)."""
+        if getattr(self, "last_sync", None) is None:
+            return 0
+        sync, npix, T = self.last_sync
+        out = torch.zeros(1, dtype=torch.int32, device=sync.device)
+        call("stf_lstm_coop_error", _p(sync), npix, T, _p(out), stream())
+        return int(out.item())
+
     def forward(self, lbuf: Feat, T, B, hT: Feat):
         C, dev = self.C, lbuf.buf.device
         L = self.lstm
@@ -201,11 +217,22 @@ class LSTMProgram:
              _p(L.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias), stream())
         cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
         fused = self.fused(lbuf, hT)
+        coop = not fused and self.coop(lbuf, hT)
         if fused:
             # all T steps in one launch: c in registers, h_{t-1} in LDS (same values)
             lbuf.check()
             hT.check()
             call("stf_lstm_seq_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs, stream())
+        elif coop:
+            # C >= 128: all T steps in one persistent launch, the C/32 workgroups of a pixel
+            # block hand h_t to each other in-launch (same values as the per-step launches)
+            lbuf.check()
+            hT.check()
+            lib = _lib.load()
+            sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
+            call("stf_lstm_coop_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs,
+                 _p(sync), stream())
+            self.last_sync = (sync, npix, T)
         else:
             for t in range(T):
                 src = rows(lbuf, t * B, B)

@@ -59,10 +59,11 @@ def _splitmix_uniform(seed, stream, n):
     return (z >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
 
 
-def splitmix_dce_case(seed, batch, time_steps, height, width):
+def splitmix_dce_case(seed, batch, time_steps, height, width, target_hw=None):
     """Deterministic CPU DCE stack + disc mask of the fixture set (tests/golden/make_golden*.py):
     background 0.5 + U(-0.3, 0.3), two discs per image whose intensity rises by 0.25 t/T, normalised
-    like train.py:147-148.  Returns (image [B, T, 1, H, W] fp32, mask [B, H, W] int64)."""
+    like train.py:147-148.  Returns (image [B, T, 1, H, W] fp32, mask [B, H, W] int64); ``target_hw``
+    nearest-downsamples the mask (STF predicts at H/2)."""
     import numpy as np
     b, t, h, w = batch, time_steps, height, width
     img = _splitmix_uniform(seed, 0, b * t * h * w).reshape(b, t, 1, h, w) * 0.3 + 0.5
@@ -76,4 +77,36 @@ def splitmix_dce_case(seed, batch, time_steps, height, width):
             mask[i][disc] = 1
             for tt in range(t):
                 img[i, tt, 0][disc] += 0.25 * (tt + 1) / t
+    if target_hw is not None:
+        mask = mask[:, :: h // target_hw[0], :: w // target_hw[1]].copy()
     return torch.from_numpy(((img - 0.709) / 0.127).astype(np.float32)), torch.from_numpy(mask)
+
+
+def canonical_state_dict(template, seed=0):
+    """Seeded, platform-independent weights with PyTorch's default-init distributions (the
+    reference relies on them: src/unet.py:12, src/stf_lstm_unet.py:13,105,124): conv / convT /
+    linear weights and biases U(-1/sqrt(fan_in), +), BatchNorm 1 / 0 / 0 / 1, LSTM U(-1/sqrt(H), +),
+    every entry drawn from the splitmix64 stream (seed, key index, element index).  The weights
+    the trained-Dice fixtures started from, so bench.py's Dice legs can restart that training
+    without committing 27 M parameters (tests/test_surface_cpu.py pins it to the fixtures' init)."""
+    import numpy as np
+    keys = list(template.keys())
+    out = {}
+    for idx, key in enumerate(keys):
+        t = template[key]
+        prefix, _, leaf = key.rpartition(".")
+        if leaf == "num_batches_tracked":
+            out[key] = torch.zeros_like(t)
+            continue
+        if (prefix + ".running_mean") in template:            # BatchNorm
+            out[key] = torch.ones_like(t) if leaf in ("weight", "running_var") else torch.zeros_like(t)
+            continue
+        if "_ih_l" in leaf or "_hh_l" in leaf:                 # nn.LSTM
+            bound = 1.0 / np.sqrt(template[prefix + ".weight_hh_l0"].shape[1])
+        else:
+            shp = tuple((template.get(prefix + ".weight") if leaf == "bias" else t).shape)
+            fan = shp[0] if len(shp) < 2 else int(np.prod(shp[1:]))
+            bound = 1.0 / np.sqrt(fan)
+        vals = _splitmix_uniform(seed, idx, t.numel()) * bound
+        out[key] = torch.from_numpy(vals.astype(np.float32)).reshape(t.shape).to(t.dtype)
+    return out

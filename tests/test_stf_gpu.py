@@ -377,6 +377,37 @@ def test_lstm_whole_sequence_equals_per_step(monkeypatch, T, B, H):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("C,T,B,H", [(128, 5, 3, 6), (256, 3, 2, 8), (512, 4, 16, 8), (128, 8, 16, 32)])
+def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
+    """stf_lstm_coop_fwd (C = 128 / 256 / 512: one persistent launch, the C/32 workgroups of a
+    64-pixel block exchanging h_t in-launch; ragged last block when B*H*H % 64 != 0; (512, 4,
+    16, 8) and (128, 8, 16, 32) are lstm4 / lstm2 of cfg3) gives bit for bit the per-step
+    launches' h_T, cell states and [x | h] rows, and no hand-off timed out; the backward that
+    follows (per-step, gates recomputed) then matches too."""
+    from stfunet import nhwc
+    from stfunet.stf_lstm_unet import LSTMProgram
+    lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
+    lbuf = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+    lbuf.buf.view(-1, 2 * C)[:, :C].normal_()
+    dhT = nhwc.new_feat(B, H, H, 3 * C, DEV).slice(C, C)
+    dhT.buf.normal_()
+    prog = LSTMProgram(lstm)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("STF_LSTM_COOP", mode)
+        lb = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+        lb.buf.copy_(lbuf.buf)
+        hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
+        st = prog.forward(lb, T, B, hT)
+        if mode == "1":
+            assert prog.coop_error() == 0
+        gv = _Grads(lstm)
+        dx = prog.backward(st, dhT, gv)
+        out[mode] = [hT.dense(), st.c, lb.buf.clone(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
+    for i, (a, b) in enumerate(zip(out["0"], out["1"])):
+        assert torch.equal(a, b), i
+
+
 def test_stf_eval_mode_backward_vs_oracle():
     """Whole-model STF backward in eval mode (BatchNorm with running statistics) vs autograd
     of the fp32 oracle: with constant statistics the bf16 error stays small, so the

@@ -121,6 +121,22 @@ def test_product_synthetic_cases_match_fixture_generator():
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
+def test_product_canonical_init_matches_fixture_init():
+    """stfunet.synthetic.canonical_state_dict (bench.py's STF Dice leg restarts the reference's
+    training from it) equals oracle.init's, which wrote the fixtures, bit for bit; and the
+    half-resolution target option equals dce_case's."""
+    from oracle.cases import dce_case
+    from oracle.init import canonical_state_dict as ref_init
+    from stfunet import STFLSTMUNet
+    from stfunet.synthetic import canonical_state_dict, splitmix_dce_case
+    tmpl = STFLSTMUNet(time_steps=4, use_pk_maps=True).state_dict()
+    a, b = canonical_state_dict(tmpl, seed=0), ref_init(tmpl, seed=0)
+    assert list(a) == list(b) and all(torch.equal(a[k], b[k]) for k in a)
+    x0, t0 = dce_case(4001, 2, 4, 64, 64, target_hw=(32, 32))
+    x1, t1 = splitmix_dce_case(4001, 2, 4, 64, 64, target_hw=(32, 32))
+    assert torch.equal(x0, x1) and torch.equal(t0, t1) and t1.shape == (2, 32, 32)
+
+
 def test_size_queries_depend_only_on_the_cached_signature():
     """nhwc.igemm / nhwc._wgrad ask stf_igemm_stat_tiles / _bnr_tiles / _ws_bytes and
     stf_wgrad_plan once per launch signature (geometry, flags, which optional pointers are

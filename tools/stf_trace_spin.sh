@@ -6,7 +6,7 @@ root=$GRAFT_REPO_ROOT
 out=$root/gpurun_out/stfspin
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/raw -o run -- python3 $root/tools/gpu_critical.py --model ${MODEL:-stf} --steps 3 > $out/crit.txt 2> $out/crit.err
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $out/raw -o run -- python3 $root/tools/gpu_critical.py --model ${MODEL:-stf} --steps 3 --spin-ms ${SPIN:-40} > $out/crit.txt 2> $out/crit.err
 f=$(find $out/raw -name 'run_kernel_trace.csv' | head -1)
 cp $f $out/kernel_trace.csv
 rm -rf $out/raw
