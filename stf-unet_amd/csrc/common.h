@@ -79,7 +79,34 @@ STF_DEV float round_e(float v) { return e2f(f2e(v)); }
 // gate recompute and the cell backward all use these, so the recomputed gates equal
 // the forward's bit for bit.
 STF_DEV float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-STF_DEV float tanh_f(float x) { return 2.f * sigm(2.f * x) - 1.f; }
+STF_DEV float tanh_f(float x) { return __builtin_fmaf(2.f, sigm(2.f * x), -1.f); }
+
+// The LSTM cell, shared by every path that computes it (the per-step GEMM epilogues, the
+// whole-sequence and the cooperative kernels, the standalone cell backward), with every
+// contraction spelled out (contract(off) + explicit fma): left to the compiler, the same
+// source expression fused differently in different kernels (register pressure decides) and
+// the paths disagreed by an ulp.  Forward: gates from pre-activations (i, f, g, o),
+// c = f c_prev + i g, h = o tanh(c).
+STF_DEV void lstm_cell_fwd(float pi, float pf, float pg, float po, float cp, float& gi, float& gf, float& gg,
+                           float& go, float& c, float& h) {
+#pragma clang fp contract(off)
+  gi = sigm(pi); gf = sigm(pf); gg = tanh_f(pg); go = sigm(po);
+  c = __builtin_fmaf(gf, cp, gi * gg);
+  h = go * tanh_f(c);
+}
+// Backward of one cell step: dct = dh o (1 - tanh^2 c) + dc_next; pre-activation gate
+// gradients (di, df, dg, do) and dc_prev = dct f.
+STF_DEV void lstm_cell_bwd(float gi, float gf, float gg, float go, float ct, float cp, float dh, float dcn,
+                           float& d_i, float& d_f, float& d_g, float& d_o, float& dcp) {
+#pragma clang fp contract(off)
+  const float tc = tanh_f(ct);
+  const float dct = __builtin_fmaf(dh * go, __builtin_fmaf(-tc, tc, 1.f), dcn);
+  d_o = ((dh * tc) * go) * (1.f - go);
+  d_i = ((dct * gg) * gi) * (1.f - gi);
+  d_g = (dct * gi) * __builtin_fmaf(-gg, gg, 1.f);
+  d_f = ((dct * cp) * gf) * (1.f - gf);
+  dcp = dct * gf;
+}
 
 // ---------------------------------------------------------------- reductions
 STF_DEV float wave_sum(float v) {

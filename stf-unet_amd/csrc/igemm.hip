@@ -82,12 +82,12 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
       if (EPI == 1) {
         // LSTM cell (torch gate order i, f, g, o): c = f*c_prev + i*g, h = o*tanh(c)
         const int ch = nb >> 2, Ch = a.Nout >> 2;
-        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-        const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
         const float cp = a.c_prev ? a.c_prev[(size_t)m * Ch + ch] : 0.f;
-        const float c = gf * cp + gi * gg;
+        float gi, gf, gg, go, c, hh;
+        lstm_cell_fwd(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3], cp,
+                      gi, gf, gg, go, c, hh);
         a.c_out[(size_t)m * Ch + ch] = c;
-        reinterpret_cast<e16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2e(go * tanh_f(c));
+        reinterpret_cast<e16*>(a.h_out)[(size_t)m * a.hcs + ch] = f2e(hh);
         if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
         continue;
       }
@@ -96,17 +96,14 @@ STF_DEV void igemm_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 1
         // dc = dh*o*(1-tanh(c)^2) + dc_next, dc_prev = dc*f, pre-activation gate gradients
         const int ch = nb >> 2, Ch = a.Nout >> 2;
         const size_t u = (size_t)m * Ch + ch;
-        const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-        const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
-        const float tc = tanh_f(a.c_out[u]);
+        float gi, gf, gg, go, cx, hx;
+        lstm_cell_fwd(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3], 0.f,
+                      gi, gf, gg, go, cx, hx);
         const float h = e2f(reinterpret_cast<const e16*>(a.l_dh)[(size_t)m * a.l_dhcs + ch]);
-        const float dc = h * go * (1.f - tc * tc) + (a.l_dcn ? a.l_dcn[u] : 0.f);
         const float cp = a.c_prev ? a.c_prev[u] : 0.f;
-        const float d_o = h * tc * go * (1.f - go);
-        const float d_i = dc * gg * gi * (1.f - gi);
-        const float d_g = dc * gi * (1.f - gg * gg);
-        const float d_f = dc * cp * gf * (1.f - gf);
-        a.l_dcp[u] = dc * gf;
+        float d_i, d_f, d_g, d_o, dcp;
+        lstm_cell_bwd(gi, gf, gg, go, a.c_out[u], cp, h, a.l_dcn ? a.l_dcn[u] : 0.f, d_i, d_f, d_g, d_o, dcp);
+        a.l_dcp[u] = dcp;
         *reinterpret_cast<uint2*>(a.l_dg + (size_t)m * a.Nout + nb) = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
         continue;
       }
@@ -327,11 +324,11 @@ STF_DEV void lstm_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / 
     for (int i = 0; i < TM; ++i) {
       const int row = wm * WTM + i * 16 + fr, m = m0 + row;
       if (!(m < m_end && nb < a.Nout)) continue;
-      const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-      const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
-      const float c = gf * cs[row * PS + hl] + gi * gg;
+      float gi, gf, gg, go, c, hh;
+      lstm_cell_fwd(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3],
+                    cs[row * PS + hl], gi, gf, gg, go, c, hh);
       cs[row * PS + hl] = c;
-      hs[row * HS + hl] = f2e(go * tanh_f(c));
+      hs[row * HS + hl] = f2e(hh);
       if (a.gates) *reinterpret_cast<float4*>(a.gates + (size_t)m * a.Nout + nb) = make_float4(gi, gf, gg, go);
     }
   }
@@ -421,17 +418,13 @@ STF_DEV void lstm_bwd_staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][B
     for (int i = 0; i < TM; ++i) {
       const int row = wm * WTM + i * 16 + fr, m = m0 + row;
       if (!(m < m_end && nb < a.Nout)) continue;
-      const float gi = sigm(acc[i][j][0] + bv[0]), gf = sigm(acc[i][j][1] + bv[1]);
-      const float gg = tanh_f(acc[i][j][2] + bv[2]), go = sigm(acc[i][j][3] + bv[3]);
-      const float tc = tanh_f(cts[row * PS + hl]);
-      const float h = e2f(dhs[row * HS + hl]);
-      const float dc = h * go * (1.f - tc * tc) + dcs[row * PS + hl];
-      const float cp = cps[row * PS + hl];
-      const float d_o = h * tc * go * (1.f - go);
-      const float d_i = dc * gg * gi * (1.f - gi);
-      const float d_g = dc * gi * (1.f - gg * gg);
-      const float d_f = dc * cp * gf * (1.f - gf);
-      dcs[row * PS + hl] = dc * gf;
+      float gi, gf, gg, go, cx, hx;
+      lstm_cell_fwd(acc[i][j][0] + bv[0], acc[i][j][1] + bv[1], acc[i][j][2] + bv[2], acc[i][j][3] + bv[3], 0.f,
+                    gi, gf, gg, go, cx, hx);
+      float d_i, d_f, d_g, d_o, dcp;
+      lstm_cell_bwd(gi, gf, gg, go, cts[row * PS + hl], cps[row * PS + hl], e2f(dhs[row * HS + hl]),
+                    dcs[row * PS + hl], d_i, d_f, d_g, d_o, dcp);
+      dcs[row * PS + hl] = dcp;
       *reinterpret_cast<uint2*>(a.l_dg + (size_t)m * a.Nout + nb) = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
     }
   }

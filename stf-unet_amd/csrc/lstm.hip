@@ -120,11 +120,11 @@ __global__ __launch_bounds__(NT, OCC) void lstm_seq_fwd_kernel(const uint16_t* _
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) {
         const int ch = wave * (C / 4) + nf * 4 + fk;
-        const float gi = sigm(acc[mf][nf][0] + bv[nf][0]), gf = sigm(acc[mf][nf][1] + bv[nf][1]);
-        const float gg = tanh_f(acc[mf][nf][2] + bv[nf][2]), go = sigm(acc[mf][nf][3] + bv[nf][3]);
-        const float c = gf * cc[mf][nf] + gi * gg;
+        float gi, gf, gg, go, c, hh;
+        lstm_cell_fwd(acc[mf][nf][0] + bv[nf][0], acc[mf][nf][1] + bv[nf][1], acc[mf][nf][2] + bv[nf][2],
+                      acc[mf][nf][3] + bv[nf][3], cc[mf][nf], gi, gf, gg, go, c, hh);
         cc[mf][nf] = c;
-        reinterpret_cast<e16*>(hs[cur ^ 1])[soff(r, ch >> 3) + (ch & 7)] = f2e(go * tanh_f(c));
+        reinterpret_cast<e16*>(hs[cur ^ 1])[soff(r, ch >> 3) + (ch & 7)] = f2e(hh);
         cs[cur][r * C + ((((ch >> 2) ^ (r & 7)) << 2) | (ch & 3))] = c;
       }
     }
@@ -302,18 +302,14 @@ __global__ __launch_bounds__(NT, 1) void lstm_seq_bwd_kernel(const uint16_t* __r
 #pragma unroll
       for (int nf = 0; nf < NF1; ++nf) {
         const int ch = wave * (C / 4) + nf * 4 + fk;
-        const float gi = sigm(acc[mf][nf][0] + bv[nf][0]), gf = sigm(acc[mf][nf][1] + bv[nf][1]);
-        const float gg = tanh_f(acc[mf][nf][2] + bv[nf][2]), go = sigm(acc[mf][nf][3] + bv[nf][3]);
+        float gi, gf, gg, go, cx, hx;
+        lstm_cell_fwd(acc[mf][nf][0] + bv[nf][0], acc[mf][nf][1] + bv[nf][1], acc[mf][nf][2] + bv[nf][2],
+                      acc[mf][nf][3] + bv[nf][3], 0.f, gi, gf, gg, go, cx, hx);
         const int co = r * C + ((((ch >> 2) ^ (r & 7)) << 2) | (ch & 3));
-        const float tc = tanh_f(ct[co]);
         const float h = e2f(reinterpret_cast<const e16*>(dhs)[r * C + ((((ch >> 3) ^ (r & 7))) << 3) + (ch & 7)]);
-        const float d = h * go * (1.f - tc * tc) + dc[mf][nf];
-        const float c1 = cp[co];
-        const float d_o = h * tc * go * (1.f - go);
-        const float d_i = d * gg * gi * (1.f - gi);
-        const float d_g = d * gi * (1.f - gg * gg);
-        const float d_f = d * c1 * gf * (1.f - gf);
-        dc[mf][nf] = d * gf;
+        float d_i, d_f, d_g, d_o, dcp;
+        lstm_cell_bwd(gi, gf, gg, go, ct[co], cp[co], h, dc[mf][nf], d_i, d_f, d_g, d_o, dcp);
+        dc[mf][nf] = dcp;
         // gate row 4ch+q of pixel r: 16-B chunk (ch >> 1) of the 4C-wide row, slot (ch & 1) * 4
         *reinterpret_cast<uint2*>(&dgs[o16(r, ch >> 1, RG) + (ch & 1) * 4]) =
             make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));

@@ -205,17 +205,11 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ gates, const floa
     const long m = u / C;
     const int c = (int)(u - m * C);
     const float4 gv = *reinterpret_cast<const float4*>(gates + m * 4 * C + 4 * c);
-    const float gi = gv.x, gf = gv.y, gg = gv.z, go = gv.w;
-    const float ct = cst[u];
-    const float tc = tanh_f(ct);
     const float h = e2f(reinterpret_cast<const e16*>(dh)[m * dhcs + c]);
-    float dc = h * go * (1.f - tc * tc) + (dc_in ? dc_in[u] : 0.f);
     const float cp = cprev ? cprev[u] : 0.f;
-    const float d_o = h * tc * go * (1.f - go);
-    const float d_i = dc * gg * gi * (1.f - gi);
-    const float d_g = dc * gi * (1.f - gg * gg);
-    const float d_f = dc * cp * gf * (1.f - gf);
-    dc_out[u] = dc * gf;
+    float d_i, d_f, d_g, d_o, dcp;
+    lstm_cell_bwd(gv.x, gv.y, gv.z, gv.w, cst[u], cp, h, dc_in ? dc_in[u] : 0.f, d_i, d_f, d_g, d_o, dcp);
+    dc_out[u] = dcp;
     const uint2 pk = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
     *reinterpret_cast<uint2*>(dgates + m * 4 * C + 4 * c) = pk;
   }

@@ -206,7 +206,7 @@ class LSTMProgram:
         call("stf_lstm_coop_error", _p(sync), npix, T, _p(out), stream())
         return int(out.item())
 
-    def forward(self, lbuf: Feat, T, B, hT: Feat):
+    def forward(self, lbuf: Feat, T, B, hT: Feat, need_bwd=True):
         C, dev = self.C, lbuf.buf.device
         L = self.lstm
         npix = B * lbuf.H * lbuf.W
@@ -230,8 +230,10 @@ class LSTMProgram:
             hT.check()
             lib = _lib.load()
             sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
+            # the activated gates (fp32) are kept for the cooperative backward (no recompute)
+            gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev) if need_bwd else None
             call("stf_lstm_coop_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs,
-                 _p(sync), stream())
+                 _p(gates), _p(sync), stream())
             self.last_sync = (sync, npix, T)
         else:
             for t in range(T):
@@ -242,6 +244,8 @@ class LSTMProgram:
         st = _S()
         st.lbuf, st.T, st.B, st.wcat, st.wcat_t, st.bias, st.c = lbuf, T, B, wcat, wcat_t, bias, cst
         st.fused = fused
+        st.coop = coop and need_bwd and os.environ.get("STF_LSTM_COOP_BWD", "1") != "0"
+        st.gates = gates if coop else None
         return st
 
     def backward(self, st, dhT: Feat, gv):
@@ -256,6 +260,15 @@ class LSTMProgram:
             dhT.check()
             call("stf_lstm_seq_bwd", _p(st.wcat), _p(st.wcat_t), _p(st.bias), lb.ptr(), npix, T, C, _p(st.c),
                  dhT.ptr(), dhT.cs, dg.ptr(), d2.ptr(), d2.cs, stream())
+        elif st.coop:
+            # C >= 128: all T steps backward in one persistent launch (dgates and [dx | dh]
+            # exchanged in-launch inside each pixel block; the forward's gates, no recompute)
+            dhT.check()
+            lib = _lib.load()
+            sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
+            call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
+                 dg.ptr(), d2.ptr(), d2.cs, _p(sync), stream())
+            self.last_sync = (sync, npix, T)
         else:
             dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
             for t in range(T - 1, -1, -1):
@@ -428,10 +441,10 @@ class STFProgram:
                 dc = dcat[2 - li] = new_feat(B, hh, ww, Cout + d.fusion.in_channels - Cout, dev)
                 side[li].wait_stream(main)
                 with torch.cuda.stream(side[li]):
-                    S.lstm[li] = lp.forward(lbuf, T, B, dc.slice(dc.C - lp.C, lp.C))
+                    S.lstm[li] = lp.forward(lbuf, T, B, dc.slice(dc.C - lp.C, lp.C), need_bwd)
             else:
                 e4f = new_feat(B, hh, ww, lp.C, dev)
-                S.lstm[li] = lp.forward(lbuf, T, B, e4f)
+                S.lstm[li] = lp.forward(lbuf, T, B, e4f, need_bwd)
         S.dcat = dcat
         # ---- decoder
         S.dec = []

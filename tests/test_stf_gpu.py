@@ -382,8 +382,11 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
     """stf_lstm_coop_fwd (C = 128 / 256 / 512: one persistent launch, the C/32 workgroups of a
     64-pixel block exchanging h_t in-launch; ragged last block when B*H*H % 64 != 0; (512, 4,
     16, 8) and (128, 8, 16, 32) are lstm4 / lstm2 of cfg3) gives bit for bit the per-step
-    launches' h_T, cell states and [x | h] rows, and no hand-off timed out; the backward that
-    follows (per-step, gates recomputed) then matches too."""
+    launches' h_T, cell states and [x | h] rows, and no hand-off timed out.  The cooperative
+    backward (stf_lstm_coop_bwd: the forward's gates, dgates and [dx | dh] exchanged in-launch)
+    gives the per-step backward's input and weight gradients: bit for bit where the per-step
+    dgates x W GEMM runs unsplit (lstm2 at cfg3), else within rel 2e-3 (small pixel counts split
+    that GEMM over K: a different fp32 summation order before the 16-bit rounding)."""
     from stfunet import nhwc
     from stfunet.stf_lstm_unet import LSTMProgram
     lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
@@ -400,12 +403,21 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
         hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
         st = prog.forward(lb, T, B, hT)
         if mode == "1":
-            assert prog.coop_error() == 0
+            assert st.coop and prog.coop_error() == 0
         gv = _Grads(lstm)
         dx = prog.backward(st, dhT, gv)
+        if mode == "1":
+            assert prog.coop_error() == 0
         out[mode] = [hT.dense(), st.c, lb.buf.clone(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
     for i, (a, b) in enumerate(zip(out["0"], out["1"])):
-        assert torch.equal(a, b), i
+        if i < 3:                                   # forward: always bitwise
+            dd = (a.float() - b.float()).abs()
+            assert torch.equal(a, b), (i, int((dd > 0).sum()), dd.max().item(), a.shape,
+                                       torch.nonzero(dd.reshape(-1) > 0)[:8].flatten().tolist())
+        else:
+            e = ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+            unsplit = (C, B * H * H) == (128, 16 * 32 * 32)      # lstm2 at cfg3: per-step GEMM not split
+            assert torch.equal(a, b) or (not unsplit and e < 2e-3), (i, e)
 
 
 def test_stf_eval_mode_backward_vs_oracle():
