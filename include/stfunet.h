@@ -382,17 +382,19 @@ int stf_lstm_seq_bwd(const void* wcat, const void* wcat_t, const float* bias, co
 size_t stf_lstm_coop_sync_bytes(int P, int T);
 int stf_lstm_coop_supported(int C);
 int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
-                      void* h_last, int h_cstride, float* gates, unsigned* sync, stf_stream_t stream);
+                      void* h_last, int h_cstride, float* gates, unsigned* sync, int max_wg, stf_stream_t stream);
 /* gates (or NULL): [T][P][4C] fp32 activated gates (i, f, g, o interleaved per channel), kept
  * for stf_lstm_coop_bwd: the BPTT of the same sequence in one persistent launch (same
  * workgroup grid; per step the C/32 workgroups of a pixel block exchange the dgates rows and
  * then [dx_t | dh_{t-1}] in-launch).  Outputs as stf_lstm_seq_bwd: dgates [T][P][4C] 16-bit,
  * dx rows [T][P] of stride dx_cstride (>= 2C) receiving [dx_t | dh_{t-1}]; dh_last = dL/dh_{T-1}.
  * Same values as the per-step path (bit for bit where its dgates x W GEMM is not split over
- * K).  `sync` as for the forward (re-zeroed by the call). */
+ * K).  `sync` as for the forward (re-zeroed by the call).  max_wg (both directions): at most this
+ * many workgroups (one per CU; 0 = one per CU of the device) -- a launch on a side stream beside
+ * other work leaves the rest of the chip to it (a group of C/32 must fit). */
 int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, int C,
                       const void* dh_last, int dh_cstride, void* dgates, void* dx, int dx_cstride,
-                      unsigned* sync, stf_stream_t stream);
+                      unsigned* sync, int max_wg, stf_stream_t stream);
 int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* out, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
 int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,

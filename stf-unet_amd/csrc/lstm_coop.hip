@@ -266,27 +266,46 @@ __global__ __launch_bounds__(CNT, 1) void lstm_coop_bwd_kernel(const uint16_t* _
 #pragma unroll
       for (int nf = 0; nf < NF; ++nf) dc[mf][nf] = 0.f;
     for (int t = T - 1; t >= 0; --t) {
+      // the forward's gates and cell states of step t need no hand-off: all in flight before
+      // the wait for dh_t (clamped addresses for rows past P: loaded, never used)
+      float4 gt[MF][NF];
+      float ct[MF][NF], c1[MF][NF];
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf) {
+        const int r = min(mf * 16 + fr, rows - 1);
+        const size_t m = (size_t)t * P + m0 + r;
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const int ch = ch0 + wave * 8 + nf * 4 + fk;
+          gt[mf][nf] = *reinterpret_cast<const float4*>(gates + m * 4 * C + ch * 4);
+          ct[mf][nf] = cst[m * C + ch];
+          c1[mf][nf] = t > 0 ? cst[(m - P) * C + ch] : 0.f;
+        }
+      }
       if (t < T - 1) wait_for(&cntB[pb * T + t + 1]);         // dh_t from step t+1's outputs
+      float hv[MF][NF];
+#pragma unroll
+      for (int mf = 0; mf < MF; ++mf) {
+        const int r = min(mf * 16 + fr, rows - 1);
+        const size_t m = (size_t)t * P + m0 + r;
+#pragma unroll
+        for (int nf = 0; nf < NF; ++nf) {
+          const int ch = ch0 + wave * 8 + nf * 4 + fk;
+          hv[mf][nf] = t == T - 1 ? e2f(reinterpret_cast<const e16*>(dhT)[(size_t)(m0 + r) * dhcs + ch])
+                                  : e2f(reinterpret_cast<const e16*>(d2)[(m + P) * d2cs + C + ch]);
+        }
+      }
       // 1. cell backward of this slice's 32 channels: lane = (pixel r, channel cl)
 #pragma unroll
       for (int mf = 0; mf < MF; ++mf) {
         const int r = mf * 16 + fr;
-        const bool ok = r < rows;
-        const size_t m = (size_t)t * P + m0 + r;
 #pragma unroll
         for (int nf = 0; nf < NF; ++nf) {
-          const int cl = wave * 8 + nf * 4 + fk, ch = ch0 + cl;
-          float4 gt = make_float4(0.f, 0.f, 0.f, 0.f);
-          float ct = 0.f, c1 = 0.f, h = 0.f;
-          if (ok) {
-            gt = *reinterpret_cast<const float4*>(gates + m * 4 * C + ch * 4);
-            ct = cst[m * C + ch];
-            if (t > 0) c1 = cst[(m - P) * C + ch];
-            h = t == T - 1 ? e2f(reinterpret_cast<const e16*>(dhT)[(size_t)(m0 + r) * dhcs + ch])
-                           : e2f(reinterpret_cast<const e16*>(d2)[(m + P) * d2cs + C + ch]);
-          }
+          const int cl = wave * 8 + nf * 4 + fk;
           float d_i, d_f, d_g, d_o, dcp;
-          lstm_cell_bwd(gt.x, gt.y, gt.z, gt.w, ct, c1, h, dc[mf][nf], d_i, d_f, d_g, d_o, dcp);
+          const float4 g4 = gt[mf][nf];
+          lstm_cell_bwd(g4.x, g4.y, g4.z, g4.w, ct[mf][nf], c1[mf][nf], hv[mf][nf], dc[mf][nf], d_i, d_f, d_g, d_o,
+                        dcp);
           dc[mf][nf] = dcp;
           *reinterpret_cast<uint2*>(&go_[r * CR + cl * 4]) = make_uint2(pack2(d_i, d_f), pack2(d_g, d_o));
         }
@@ -362,10 +381,11 @@ int num_cus() {
 }
 
 template <int C>
-int grid_of(int P) {
+int grid_of(int P, int max_wg) {
   constexpr int S = 4 * C / CR;
   const int npb = (P + CBM - 1) / CBM;
-  int groups = num_cus() / S;
+  const int budget = max_wg > 0 && max_wg < num_cus() ? max_wg : num_cus();
+  int groups = budget / S;
   if (groups < 1) groups = 1;
   if (groups > npb) groups = npb;
   return groups * S;
@@ -373,13 +393,13 @@ int grid_of(int P) {
 
 template <int C>
 int launch_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, float* c_out, void* h_last,
-               int h_cstride, float* gates, unsigned* sync, hipStream_t s) {
+               int h_cstride, float* gates, unsigned* sync, int max_wg, hipStream_t s) {
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;      // counters + the error word
   hipError_t e = hipMemsetAsync(sync, 0, ((words * 4 + 15) / 16) * 16, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_coop_fwd_kernel<C>), dim3(grid_of<C>(P)), dim3(CNT), 0, s, (const uint16_t*)wcat, bias,
+  hipLaunchKernelGGL((lstm_coop_fwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat, bias,
                      (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride, gates, sync,
                      sync + 2 * (size_t)npb * T);
   STF_CHECK_LAUNCH();
@@ -388,13 +408,13 @@ int launch_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, fl
 
 template <int C>
 int launch_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, const void* dh_last,
-               int dh_cstride, void* dgates, void* dx, int dx_cstride, unsigned* sync, hipStream_t s) {
+               int dh_cstride, void* dgates, void* dx, int dx_cstride, unsigned* sync, int max_wg, hipStream_t s) {
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;
   hipError_t e = hipMemsetAsync(sync, 0, ((words * 4 + 15) / 16) * 16, s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL((lstm_coop_bwd_kernel<C>), dim3(grid_of<C>(P)), dim3(CNT), 0, s, (const uint16_t*)wcat_t, gates,
+  hipLaunchKernelGGL((lstm_coop_bwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat_t, gates,
                      c_all, P, T, (const uint16_t*)dh_last, dh_cstride, (uint16_t*)dgates, (uint16_t*)dx, dx_cstride,
                      sync, sync + 2 * (size_t)npb * T);
   STF_CHECK_LAUNCH();
@@ -411,7 +431,8 @@ extern "C" size_t stf_lstm_coop_sync_bytes(int P, int T) {
 extern "C" int stf_lstm_coop_supported(int C) { return C == 128 || C == 256 || C == 512; }
 
 extern "C" int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
-                                 void* h_last, int h_cstride, float* gates, unsigned* sync, stf_stream_t stream) {
+                                 void* h_last, int h_cstride, float* gates, unsigned* sync, int max_wg,
+                                 stf_stream_t stream) {
   if (P <= 0 || T <= 0) return 0;
   if (!stf_lstm_coop_supported(C) || !wcat || !bias || !lbuf || !c_out || !h_last || !sync || h_cstride < C ||
       h_cstride % 8)
@@ -422,15 +443,15 @@ extern "C" int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf
   if ((size_t)T * P * 2 * C * 2 >= 0xFFFFFF00ull) return STF_EINVAL;     // 32-bit buffer offsets
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
-    case 128: return launch_fwd<128>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, s);
-    case 256: return launch_fwd<256>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, s);
-    default: return launch_fwd<512>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, s);
+    case 128: return launch_fwd<128>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
+    case 256: return launch_fwd<256>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
+    default: return launch_fwd<512>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
   }
 }
 
 extern "C" int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, int C,
                                  const void* dh_last, int dh_cstride, void* dgates, void* dx, int dx_cstride,
-                                 unsigned* sync, stf_stream_t stream) {
+                                 unsigned* sync, int max_wg, stf_stream_t stream) {
   if (P <= 0 || T <= 0) return 0;
   if (!stf_lstm_coop_supported(C) || !wcat_t || !gates || !c_all || !dh_last || !dgates || !dx || !sync ||
       dh_cstride < C || dx_cstride < 2 * C || dx_cstride % 8)
@@ -442,9 +463,9 @@ extern "C" int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const f
     return STF_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
-    case 128: return launch_bwd<128>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, s);
-    case 256: return launch_bwd<256>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, s);
-    default: return launch_bwd<512>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, s);
+    case 128: return launch_bwd<128>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
+    case 256: return launch_bwd<256>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
+    default: return launch_bwd<512>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
   }
 }
 

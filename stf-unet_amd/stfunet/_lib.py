@@ -102,8 +102,8 @@ _SIGS = {
     "stf_eval_counts": (c_int, [P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_lstm_coop_sync_bytes": (c_size_t, [c_int, c_int]),
     "stf_lstm_coop_supported": (c_int, [c_int]),
-    "stf_lstm_coop_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, P]),
-    "stf_lstm_coop_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, c_int, P, P, c_int, P, P]),
+    "stf_lstm_coop_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P]),
+    "stf_lstm_coop_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, P]),
     "stf_lstm_coop_error": (c_int, [P, c_int, c_int, P, P]),
     "stf_eval_counts_sm": (c_int, [P, P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_tofts_forward": (c_int, [P, P, P, c_int, c_int, P, P, P, P, P, c_int, c_float, P, P]),

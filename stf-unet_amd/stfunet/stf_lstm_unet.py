@@ -180,9 +180,12 @@ class LSTMProgram:
     its epilogue, instead of storing T x P x 4C fp32 activated gates.
     """
 
-    def __init__(self, lstm):
+    def __init__(self, lstm, max_wg=0):
         self.lstm = lstm
         self.C = lstm.hidden_size
+        # workgroup budget of the cooperative kernels (one per CU; 0 = the whole chip): an LSTM
+        # on a side stream leaves the rest to the encoder / decoder of the main stream
+        self.max_wg = max_wg
 
     def fused(self, lbuf: Feat, hT: Feat):
         """Whole-sequence kernel (stf_lstm_seq_fwd) for this hidden size and layout?
@@ -192,8 +195,16 @@ class LSTMProgram:
 
     def coop(self, lbuf: Feat, hT: Feat):
         """Cooperative whole-sequence forward (stf_lstm_coop_fwd, C = 128 / 256 / 512)?
-        STF_LSTM_COOP=0 keeps the per-step launches (A/B)."""
-        return (os.environ.get("STF_LSTM_COOP", "1") != "0" and bool(_lib.load().stf_lstm_coop_supported(self.C))
+        STF_LSTM_COOP: 1 = every supported C, 0 = the per-step launches, or a comma list of
+        hidden sizes ("512", the default: only lstm4, the one on the main stream).
+        STF_LSTM_COOP_BWD=1 also runs the cooperative backward (off by default, see above)."""
+        # default: lstm4 only (the main-stream LSTM).  Measured (same box, cfg3, round 3): coop
+        # forward of lstm4 +1.0 %; coop lstm2 / lstm3 on their side streams -0.5..-4 % (a launch
+        # that needs its whole group resident spins on CUs the encoder needs); coop backward
+        # -0.4..-2 % (lstm3's and lstm4's backward start together and contend)
+        mode = os.environ.get("STF_LSTM_COOP", "512")
+        on = mode == "1" or (mode not in ("0", "") and str(self.C) in mode.split(","))
+        return (on and bool(_lib.load().stf_lstm_coop_supported(self.C))
                 and lbuf.off == 0 and lbuf.cs == 2 * self.C and hT.cs >= self.C and hT.cs % 8 == 0
                 and hT.ptr() % 16 == 0)
 
@@ -233,7 +244,7 @@ class LSTMProgram:
             # the activated gates (fp32) are kept for the cooperative backward (no recompute)
             gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev) if need_bwd else None
             call("stf_lstm_coop_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs,
-                 _p(gates), _p(sync), stream())
+                 _p(gates), _p(sync), self.max_wg, stream())
             self.last_sync = (sync, npix, T)
         else:
             for t in range(T):
@@ -244,7 +255,7 @@ class LSTMProgram:
         st = _S()
         st.lbuf, st.T, st.B, st.wcat, st.wcat_t, st.bias, st.c = lbuf, T, B, wcat, wcat_t, bias, cst
         st.fused = fused
-        st.coop = coop and need_bwd and os.environ.get("STF_LSTM_COOP_BWD", "1") != "0"
+        st.coop = coop and need_bwd and os.environ.get("STF_LSTM_COOP_BWD", "0") == "1"
         st.gates = gates if coop else None
         return st
 
@@ -267,7 +278,7 @@ class LSTMProgram:
             lib = _lib.load()
             sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
             call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
-                 dg.ptr(), d2.ptr(), d2.cs, _p(sync), stream())
+                 dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, stream())
             self.last_sync = (sync, npix, T)
         else:
             dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
@@ -311,7 +322,8 @@ class STFProgram:
         fr = m.final_res
         self.final_res = ResBlockProgram(fr.conv_block[0], fr.conv_block[1], fr.conv_block[3], fr.conv_block[4])
         self.lstms = [m.lstm1, m.lstm2, m.lstm3, m.lstm4]
-        self.lstm_progs = [LSTMProgram(lstm) for lstm in self.lstms]
+        side_wg = int(os.environ.get("STF_LSTM_SIDE_WG", "64"))
+        self.lstm_progs = [LSTMProgram(lstm, side_wg if k < 3 else 0) for k, lstm in enumerate(self.lstms)]
         self._side = None
         self._wstream = None
 

@@ -396,6 +396,7 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
     dhT.buf.normal_()
     prog = LSTMProgram(lstm)
     out = {}
+    monkeypatch.setenv("STF_LSTM_COOP_BWD", "1")
     for mode in ("0", "1"):
         monkeypatch.setenv("STF_LSTM_COOP", mode)
         lb = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
@@ -418,6 +419,32 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
             e = ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
             unsplit = (C, B * H * H) == (128, 16 * 32 * 32)      # lstm2 at cfg3: per-step GEMM not split
             assert torch.equal(a, b) or (not unsplit and e < 2e-3), (i, e)
+
+
+def test_stf_model_with_cooperative_lstms_matches_per_step(monkeypatch):
+    """The whole STF training step with every LSTM on the cooperative kernels (forward and
+    backward, STF_LSTM_COOP=1, STF_LSTM_COOP_BWD=1) against the same step on the per-step
+    launches: logits and loss bit for bit (the forward is), every parameter gradient within
+    rel 1e-2 (the per-step dgates x W GEMMs split over K at these small sizes)."""
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    g = np.load(os.path.join(GOLDEN, "stf_t4.npz"))
+    x, t = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["target"]).to(DEV)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("STF_LSTM_COOP", mode)
+        monkeypatch.setenv("STF_LSTM_COOP_BWD", mode)
+        m = STFLSTMUNet(time_steps=4)
+        m.load_state_dict(canonical_state_dict(m.state_dict(), seed=0))
+        m = m.to(DEV).train()
+        out = m(x)["out"]
+        loss = criterion({"out": out}, t)
+        loss.backward()
+        res[mode] = (out.detach(), loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    assert torch.equal(res["0"][0], res["1"][0]) and res["0"][1] == res["1"][1]
+    for k, g0 in res["0"][2].items():
+        assert rel(res["1"][2][k], g0) < 1e-2, k
 
 
 def test_stf_eval_mode_backward_vs_oracle():
