@@ -7,7 +7,7 @@
 #   4. the PK-map fit bench (tools/bench_pk.py) under rocprofv3, the eval-metric micro-bench
 # Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
 set -e
-tag=${1:-r02}
+tag=${1:-r03}
 root=$GRAFT_REPO_ROOT
 out=$root/gpurun_out/prof_$tag
 mkdir -p $out
