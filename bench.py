@@ -331,7 +331,7 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
-    from stfunet import engine, nhwc
+    from stfunet import engine, nhwc, plan
     from stfunet.ddp import GradAllReduce
     from stfunet.flops import stf_train_flops, unet_train_flops
     from stfunet.optim import AdamW
@@ -412,6 +412,7 @@ def main():
         from stfunet.graph import TrainStepGraph
         loss = None                           # drop the last eager step's autograd graph before capture
         gstep = TrainStepGraph(model, opt, engine.criterion, *batches[0]).capture()
+    runtime = model.program.runtime
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -420,7 +421,11 @@ def main():
             sched.step()
             continue
         if dominant is not None and i == args.steps - 1:
-            nhwc.TIMER = nhwc.KernelTimer(only=dominant)
+            if runtime.fwd is not None:       # native plan replays: events around that kernel's ranges
+                plan.TIMED = dominant
+                runtime.timing()              # drop anything timed before
+            else:
+                nhwc.TIMER = nhwc.KernelTimer(only=dominant)
         loss = train_step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
@@ -434,6 +439,12 @@ def main():
         torch.cuda.synchronize()
     kt = nhwc.TIMER.summary() if nhwc.TIMER is not None else {}
     nhwc.TIMER = None
+    if plan.TIMED is not None:
+        n, ms, fl = runtime.timing()
+        plan.TIMED = None
+        if n:
+            kt = {dominant: dict(launches=n, ms=ms, flops=fl, avg_us=1e3 * ms / n,
+                                 tflops=fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0)}
     last_loss = float(loss.item())
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -457,7 +468,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
-            "execution": "hip_graph" if gstep is not None else "eager",
+            "execution": ("hip_graph" if gstep is not None else
+                          "native_plan" if runtime.fwd is not None else "eager"),
             "config": {"workload": workload,
                        "model": "UNet" if args.model == "unet" else "STFLSTMUNet",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,

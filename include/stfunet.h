@@ -493,6 +493,46 @@ int stf_augment_frames(const uint8_t* src, const stf_aug_frame* frames, int n, c
 int stf_augment_masks(const uint8_t* src, const stf_aug_frame* masks, int n, const int* tabs,
                       int max_out_px, int64_t* out, stf_stream_t stream);
 
+/* ---------------------------------------------------------------- launch plans
+ * The native step runtime behind the models' forward / backward (stfunet/plan.py).
+ * The reference's step is Python issuing one PyTorch op per layer and per LSTM time
+ * step (src/stf_lstm_unet.py:168-254 forward, its autograd backward;
+ * train_utils/train_and_eval.py:384-404); here the first steps of a shape run the
+ * programs' schedule from Python and one of them RECORDS it: while a plan records on
+ * the calling thread, every launch, async memset / device copy and stream wait of
+ * this library executes as usual and is appended to the plan with its final
+ * arguments (tile choices, split plans, workspace pointers resolved).  Later steps
+ * replay ranges of it with stf_plan_replay: the same kernels, streams and events,
+ * bit for bit the recorded step's results, no per-launch host logic.  The caller
+ * keeps every buffer the recorded step touched alive at its address.
+ * These are the only entry points that keep state: a plan owns its ops and events
+ * (stf_plan_destroy frees them); the recording flag is per host thread.
+ *
+ * stf_plan_tag(name, flops) / stf_plan_tag_end(): while recording, mark the ops of
+ * the following C-ABI call (a kernel family and its algorithmic FLOPs: bench.py's
+ * roofline); stf_plan_replay(.., timed_tag) brackets every range with that name by
+ * HIP events on its stream, stf_plan_timing sums them (and synchronizes).
+ * stf_stream_wait: `waiter` waits for the work enqueued on `waitee` so far (an
+ * event record + stream wait; recorded like a launch).
+ * stf_memset / stf_copy_rows (dst[r][0:cols] = src[r][0:cols], fp32, row strides in
+ * elements) / stf_i64_add_batch (*ptrs[i] += inc: BatchNorm num_batches_tracked):
+ * the step's remaining tensor ops as plan-recordable launches. */
+typedef struct stf_plan stf_plan;
+stf_plan* stf_plan_create(void);
+void stf_plan_destroy(stf_plan* plan);
+int stf_plan_record(stf_plan* plan);
+int stf_plan_stop(void);
+int stf_plan_size(const stf_plan* plan);
+int stf_plan_tag(const char* name, double flops);
+int stf_plan_tag_end(void);
+int stf_plan_replay(stf_plan* plan, int first, int last, const char* timed_tag);
+int stf_plan_timing(stf_plan* plan, int* launches, double* ms, double* flops);
+int stf_stream_wait(stf_stream_t waiter, stf_stream_t waitee);
+int stf_memset(void* p, int value, size_t bytes, stf_stream_t stream);
+int stf_copy_rows(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int rows, int cols,
+                  stf_stream_t stream);
+int stf_i64_add_batch(int64_t* const* ptrs, int count, int64_t inc, stf_stream_t stream);
+
 const char* stf_error_string(int code);
 int stf_abi_version(void);
 

@@ -11,6 +11,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+#include <type_traits>
+#include <utility>
+
 #ifdef STF_FP16
 typedef _Float16 e16;
 #else
@@ -142,6 +146,67 @@ STF_DEV double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// ---------------------------------------------------------------- launch plans
+// Every launch of the library goes through stf::launch (hipLaunchKernelGGL is redefined
+// below), and every async memset / copy through stf::memset_async / memcpy_async.  While a
+// plan records on the calling thread (stf_plan_record, plan.hip), each one is executed AND
+// appended to the plan with its final kernel arguments by value, so the whole step (the
+// host-side tile choice, plans and size queries included) replays from C++ with one call
+// per segment (stf_plan_replay): no Python, no ctypes, no re-planning.
+namespace stf {
+struct PlanOp {
+  virtual ~PlanOp() {}
+  virtual hipError_t run() const = 0;
+};
+bool plan_recording();              // a plan records on this thread
+void plan_append(PlanOp* op, hipStream_t s);   // the recording plan takes ownership
+
+template <class... A>
+struct KernelOp final : PlanOp {
+  const void* fn;
+  dim3 grid, block;
+  unsigned shmem;
+  hipStream_t stream;
+  std::tuple<A...> args;
+  template <class... B>
+  KernelOp(const void* f, dim3 g, dim3 b, unsigned sh, hipStream_t s, B&&... a)
+      : fn(f), grid(g), block(b), shmem(sh), stream(s), args(std::forward<B>(a)...) {}
+  hipError_t run() const override {
+    return std::apply(
+        [this](const A&... a) {
+          void* p[sizeof...(A) + 1] = {const_cast<void*>(static_cast<const void*>(&a))...};
+          return hipLaunchKernel(fn, grid, block, p, shmem, stream);
+        },
+        args);
+  }
+};
+
+template <class... A, class... B>
+inline void launch(void (*k)(A...), dim3 g, dim3 b, unsigned sh, hipStream_t s, B&&... args) {
+  static_assert(sizeof...(A) == sizeof...(B), "kernel argument count");
+  if (!plan_recording()) {
+    // the kernel's own parameter types, converted exactly as a <<<>>> launch converts them
+    std::tuple<std::decay_t<A>...> t(std::forward<B>(args)...);
+    std::apply(
+        [&](auto&... a) {
+          void* p[sizeof...(A) + 1] = {static_cast<void*>(&a)...};
+          (void)hipLaunchKernel((const void*)k, g, b, p, sh, s);
+        },
+        t);
+    return;
+  }
+  auto* op = new KernelOp<std::decay_t<A>...>((const void*)k, g, b, sh, s, std::forward<B>(args)...);
+  (void)op->run();
+  plan_append(op, s);
+}
+
+hipError_t memset_async(void* p, int value, size_t bytes, hipStream_t s);
+hipError_t memcpy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
+}  // namespace stf
+
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(K, G, B, SH, S, ...) ::stf::launch(K, G, B, SH, S, ##__VA_ARGS__)
 
 // ---------------------------------------------------------------- error plumbing
 #define STF_CHECK_LAUNCH() do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

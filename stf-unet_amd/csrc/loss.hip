@@ -338,10 +338,10 @@ extern "C" int stf_head_bwd(const float* dlogits, const void* y, int N, int H, i
   hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, S, HC,
                      head_partial + (size_t)tiles * HC);
   STF_CHECK_LAUNCH();
-  hipError_t e = hipMemcpyAsync(dw, head_partial + (size_t)tiles * HC, sizeof(float) * classes * C,
+  hipError_t e = stf::memcpy_async(dw, head_partial + (size_t)tiles * HC, sizeof(float) * classes * C,
                                 hipMemcpyDeviceToDevice, s);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(db, head_partial + (size_t)tiles * HC + classes * C, sizeof(float) * classes,
+    e = stf::memcpy_async(db, head_partial + (size_t)tiles * HC + classes * C, sizeof(float) * classes,
                        hipMemcpyDeviceToDevice, s);
   return (int)e;
 }

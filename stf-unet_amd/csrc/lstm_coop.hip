@@ -397,7 +397,7 @@ int launch_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, fl
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;      // counters + the error word
-  hipError_t e = hipMemsetAsync(sync, 0, ((words * 4 + 15) / 16) * 16, s);
+  hipError_t e = stf::memset_async(sync, 0, ((words * 4 + 15) / 16) * 16, s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_coop_fwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat, bias,
                      (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride, gates, sync,
@@ -412,7 +412,7 @@ int launch_bwd(const void* wcat_t, const float* gates, const float* c_all, int P
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;
-  hipError_t e = hipMemsetAsync(sync, 0, ((words * 4 + 15) / 16) * 16, s);
+  hipError_t e = stf::memset_async(sync, 0, ((words * 4 + 15) / 16) * 16, s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_coop_bwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat_t, gates,
                      c_all, P, T, (const uint16_t*)dh_last, dh_cstride, (uint16_t*)dgates, (uint16_t*)dx, dx_cstride,
@@ -471,5 +471,5 @@ extern "C" int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const f
 
 extern "C" int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* out, stf_stream_t stream) {
   const size_t npb = (size_t)(P + CBM - 1) / CBM;
-  return (int)hipMemcpyAsync(out, sync + 2 * npb * T, 4, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  return (int)stf::memcpy_async(out, sync + 2 * npb * T, 4, hipMemcpyDeviceToDevice, (hipStream_t)stream);
 }

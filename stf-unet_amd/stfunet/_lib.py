@@ -120,6 +120,20 @@ _SIGS = {
     "stf_lstm_seq_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P]),
     "stf_lstm_cell_bwd": (c_int, [P, P, P, P, c_int, P, P, P, c_int64, c_int, P]),
     "stf_pk_resize": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P]),
+    "stf_plan_create": (c_void_p, []),
+    "stf_plan_destroy": (None, [P]),
+    "stf_plan_record": (c_int, [P]),
+    "stf_plan_stop": (c_int, []),
+    "stf_plan_size": (c_int, [P]),
+    "stf_plan_tag": (c_int, [ctypes.c_char_p, ctypes.c_double]),
+    "stf_plan_tag_end": (c_int, []),
+    "stf_plan_replay": (c_int, [P, c_int, c_int, ctypes.c_char_p]),
+    "stf_plan_timing": (c_int, [P, ctypes.POINTER(c_int), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double)]),
+    "stf_stream_wait": (c_int, [P, P]),
+    "stf_memset": (c_int, [P, c_int, c_size_t, P]),
+    "stf_copy_rows": (c_int, [P, c_int64, P, c_int64, c_int, c_int, P]),
+    "stf_i64_add_batch": (c_int, [ctypes.POINTER(c_void_p), c_int, c_int64, P]),
     "stf_error_string": (ctypes.c_char_p, [c_int]),
     "stf_abi_version": (c_int, []),
     "stf_storage_type": (c_int, []),

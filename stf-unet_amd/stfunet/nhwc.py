@@ -155,14 +155,47 @@ class Feat:
         return v[..., self.off: self.off + self.C].permute(0, 3, 1, 2).float()
 
 
+# While a launch plan records (stfunet/plan.py): every buffer the step allocates is
+# appended here and stays alive with the plan, whose ops hold its address
+KEEP = None
+RECORDING = False
+
+
+def empty(shape, dtype, device):
+    """torch.empty for the programs' buffers (kept alive while a plan records)."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if KEEP is not None:
+        KEEP.append(t)
+    return t
+
+
+def memset0(t):
+    """Zero a device tensor's storage with a library launch (plan-recordable)."""
+    call("stf_memset", t.data_ptr(), 0, t.numel() * t.element_size(), stream())
+    return t
+
+
+def wait(waiter, waitee):
+    """Stream ``waiter`` waits for the work enqueued on ``waitee`` so far (torch Streams;
+    an event record + stream wait inside the library, so a recording plan keeps it)."""
+    call("stf_stream_wait", waiter.cuda_stream, waitee.cuda_stream)
+
+
+def copy_rows(src, src_ld, dst, dst_ld, rows, cols):
+    """dst[r][:cols] = src[r][:cols] for fp32 row-major tensors (row strides in elements)."""
+    assert src.dtype == torch.float32 and dst.dtype == torch.float32
+    assert src.numel() >= (rows - 1) * src_ld + cols and dst.numel() >= (rows - 1) * dst_ld + cols
+    call("stf_copy_rows", src.data_ptr(), src_ld, dst.data_ptr(), dst_ld, rows, cols, stream())
+
+
 def new_feat(N, H, W, C, device, cs=None):
     cs = cs or C
-    return Feat(torch.empty(N * H * W * cs, dtype=sdt(), device=device), N, H, W, C, cs, 0)
+    return Feat(empty(N * H * W * cs, sdt(), device), N, H, W, C, cs, 0)
 
 
 def zeros_feat(N, H, W, C, device, cs=None):
     cs = cs or C
-    return Feat(torch.zeros(N * H * W * cs, dtype=sdt(), device=device), N, H, W, C, cs, 0)
+    return Feat(memset0(empty(N * H * W * cs, sdt(), device)), N, H, W, C, cs, 0)
 
 
 # ------------------------------------------------------------------ packs
@@ -229,6 +262,9 @@ class PackCache:
             t = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
             self._desc = (self.recorded, t, mx, tiles)
         _, t, mx, tiles = self._desc
+        if KEEP is not None:       # a recording plan's pack launch reads these
+            KEEP.append(t)
+            KEEP.extend(self.bufs[k][1] for k in self.recorded)
         if tiles > 0:           # LDS-tiled transposes (every descriptor qualifies)
             call("stf_pack_weights_tiled", _p(t), len(self.recorded), tiles, stream())
         else:
@@ -247,6 +283,8 @@ class PackCache:
         if key not in self.fresh:
             _pack_into(w, mode, cpad, ent[1])
             self.fresh.add(key)
+        if KEEP is not None:
+            KEEP.append(ent[1])
         return ent[1]
 
 
@@ -342,10 +380,10 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         q = _QUERIES[qkey] = (tq, _ws_bytes_with(a, want_stats))
     tiles, nb = q
     if bnr is not None:
-        stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
+        stats = empty(groups * tiles * 2 * nout, torch.float32, dst.buf.device)
         epi.partial = stats.data_ptr()
     if want_stats:
-        stats = torch.empty(groups * tiles * 2 * nout, dtype=torch.float32, device=dst.buf.device)
+        stats = empty(groups * tiles * 2 * nout, torch.float32, dst.buf.device)
         a.stats = stats.data_ptr()
     t = TIMER
     if t is not None:
@@ -356,14 +394,25 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
             t = None
     ws = None
     if nb:
-        ws = torch.empty(nb // 4, dtype=torch.float32, device=dst.buf.device)
+        ws = empty(nb // 4, torch.float32, dst.buf.device)
         a.ws = ws.data_ptr()
     ev = t.begin() if t is not None else None
+    if RECORDING:        # name the launch range for the plan's timed replays (bench roofline)
+        _plan_tag(a, "stf_igemm_kernel_name",
+                  ("i", src.N, src.H, src.W, src.C, Hd, Wd, nout, R, S, stride, pad, transposed, scatter2x2,
+                   lstm is not None, groups, bnr is not None, want_stats),
+                  2.0 * src.N * Hd * Wd * nout * R * S * src.C / (stride * stride if transposed else 1))
     call("stf_igemm", ctypes.byref(a), stream())
+    if RECORDING:
+        call("stf_plan_tag_end")
     if t is not None:
         macs = src.N * Hd * Wd * nout * R * S * src.C
         t.end(ev, name, 2.0 * macs / (stride * stride if transposed else 1))
     return stats, tiles
+
+
+def _plan_tag(a, fn, key, flops):
+    call("stf_plan_tag", _kernel_name(fn, key, a).encode(), float(flops))
 
 
 def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None):
@@ -413,9 +462,7 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
         main = WGRAD_MAIN
         if main is None or _lib.stream() != main.cuda_stream:   # e.g. called on another side stream
             main = torch.cuda.current_stream()
-        ev = _sync_event()
-        ev.record(main)
-        side.wait_event(ev)
+        call("stf_stream_wait", side.cuda_stream, main.cuda_stream)
         dy.buf.record_stream(side)
         x.buf.record_stream(side)
         _set_stream(side)
@@ -430,18 +477,6 @@ def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):
 
 
 WGRAD_MAIN = None     # the program's main stream while WGRAD_STREAM is set
-_EVENTS = []
-_EV_NEXT = [0]
-
-
-def _sync_event():
-    """Cross-stream sync events, reused round robin: a stream wait enqueued on an event
-    keeps waiting for the record it saw, so re-recording one later is safe."""
-    if len(_EVENTS) < 64:
-        _EVENTS.append(torch.cuda.Event())
-        return _EVENTS[-1]
-    i = _EV_NEXT[0] = (_EV_NEXT[0] + 1) % len(_EVENTS)
-    return _EVENTS[i]
 
 
 def _set_stream(s):
@@ -473,7 +508,7 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
         call("stf_wgrad_plan", ctypes.byref(a), ctypes.byref(splits), ctypes.byref(nbytes))
         plan = _PLANS[pkey] = (splits.value, nbytes.value)
     splits, nbytes = plan
-    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=out.device)
+    ws = empty(nbytes // 4, torch.float32, out.device)
     a.ws = ws.data_ptr()
     a.splits = splits
     t = TIMER
@@ -482,7 +517,12 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
         if not t.wants(name):
             t = None
     ev = t.begin() if t is not None else None
+    if RECORDING:
+        _plan_tag(a, "stf_wgrad_kernel_name", ("w", x.N, x.H, x.W, x.C, dy.H, dy.W, dy.C, R, S, stride, pad),
+                  2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad", ctypes.byref(a), stream())
+    if RECORDING:
+        call("stf_plan_tag_end")
     if t is not None:
         t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
     call("stf_wgrad_reduce", ws.data_ptr(), splits, dy.C, R, S, x.C, out.data_ptr(), stream())
@@ -491,7 +531,7 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
 def channel_sum(x: Feat, out):
     x.check()
     tiles = min(1024, max(1, (x.M * (x.C // 8) + 255) // 256))
-    part = torch.empty(tiles * x.C, dtype=torch.float32, device=out.device)
+    part = empty(tiles * x.C, torch.float32, out.device)
     call("stf_channel_sum", x.ptr(), x.cs, x.M, x.C, _p(part), _p(out), stream())
 
 
@@ -501,7 +541,7 @@ class BNState:
     __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups", "training")
 
     def __init__(self, C, device, M, groups=1, training=True):
-        t = torch.empty(4, groups, C, dtype=torch.float32, device=device)
+        t = empty((4, groups, C), torch.float32, device)
         self.mean, self.invstd, self.scale, self.shift = t.unbind(0)
         self.M = M
         self.groups = groups
@@ -545,7 +585,8 @@ def flush_batches_tracked():
         call("stf_bn_running_batch", arr, len(_RUN_PENDING), stream())
         _RUN_PENDING.clear()
     for inc, ts in _NBT_PENDING.items():
-        torch._foreach_add_(ts, inc)
+        arr = (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+        call("stf_i64_add_batch", arr, len(ts), inc, stream())
     _NBT_PENDING.clear()
 
 
@@ -617,7 +658,7 @@ def bn_backward(y: Feat, st: BNState, bn, dgamma, dbeta, dz: Feat = None, dpool:
     dev = y.buf.device
     G = st.groups
     tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, G, int(dpool is not None))
-    part = torch.empty(G * tiles * 2 * C, dtype=torch.float32, device=dev)
+    part = empty(G * tiles * 2 * C, torch.float32, dev)
     if dz is not None:
         dz.check()
         assert (dz.N, dz.H, dz.W, dz.C) == (y.N, y.H, y.W, C)
@@ -669,7 +710,7 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         # gradient instead of summing the rounded dy (the reference's autograd returns
         # fp32 noise around 0 there)
         dbias = None
-    coef = torch.empty(G * 3 * C, dtype=torch.float32, device=dev)
+    coef = empty(G * 3 * C, torch.float32, dev)
     if G > 1 and (dgamma is not None or dbeta is not None):
         # grouped: the per-group sums stay parked; flush_bn_grads() adds them up for
         # every pending BatchNorm in one launch
@@ -687,7 +728,7 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         cv[:, 1:].zero_()
     bpart = None
     if dbias is not None:
-        bpart = torch.empty(_lib.load().stf_bn_bwd_apply_tiles(y.M, C) * C, dtype=torch.float32, device=dev)
+        bpart = empty(_lib.load().stf_bn_bwd_apply_tiles(y.M, C) * C, torch.float32, dev)
     dst = out if out is not None else g
     if out is not None:
         out.check()

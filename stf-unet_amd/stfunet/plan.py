@@ -1,0 +1,233 @@
+"""Native step runtime: a program's forward / backward recorded once, replayed from C++.
+
+The reference's training step is Python issuing PyTorch ops layer by layer (and, in
+``STFLSTMUNet``, time step by time step: ``src/stf_lstm_unet.py:168-254``).  The
+programs here (``UNetProgram``, ``STFProgram``) issue the same step as a schedule of
+C-ABI calls from Python: ~500 calls / ~600 launches per STF step, ~7 ms of host time
+(DESIGN.md section 5).  ``StepRuntime`` takes that Python out of the steady state:
+
+  * the first ``warm`` training steps of a shape run the schedule eagerly (the weight
+    pack list, the size queries and the code objects settle);
+  * the next one RECORDS it: the schedule runs as usual while the library appends every
+    launch, memset, device copy and cross-stream wait -- with its final arguments -- to
+    a native plan (``stf_plan_record``, csrc/plan.hip); every buffer the step allocates
+    is kept alive by the runtime (``nhwc.KEEP``, from a private memory pool), so no
+    address the plan holds is ever handed to anyone else;
+  * later steps copy the input (and, in backward, the incoming logits gradient) into the
+    recorded static buffers and replay the plan with one C call per segment
+    (``stf_plan_replay``): the same kernels, streams, events and buffers, bit for bit
+    the eager step's results.  Backward segments end where the data-parallel hook must
+    see a finished gradient bucket (``grad_ready_hook``), which runs live in Python.
+
+Anything that changes what the step would launch -- shapes, train / eval, storage
+dtype, the current stream, parameter or buffer addresses, the gradient buffer, a DDP
+hook appearing -- changes the signature and the plan is recorded again.  The forward
+returns the recorded (static) logits tensor, as a captured graph does: a step's logits
+are overwritten by the next step's forward.
+
+``STF_PLAN=0`` keeps every step eager (A/B, debugging); ``STF_PLAN_WARM`` sets the
+number of eager steps before recording (default 1).
+"""
+import ctypes
+import os
+import weakref
+
+import torch
+
+from . import _lib, nhwc
+from ._lib import call
+
+TIMED = None           # kernel name whose ranges replays bracket with HIP events (bench.py)
+
+
+def enabled():
+    # a HIP-graph capture (stfunet/graph.py) records the eager launches itself
+    return os.environ.get("STF_PLAN", "1") != "0" and not torch.cuda.is_current_stream_capturing()
+
+
+class Plan:
+    """One recorded launch sequence (a ``stf_plan``) in the active storage's library."""
+
+    def __init__(self):
+        self.lib = _lib.load()
+        self.h = self.lib.stf_plan_create()
+        if not self.h:
+            raise MemoryError("stf_plan_create failed")
+        self.n = 0
+
+    def record(self, fn):
+        _lib.check(self.lib.stf_plan_record(self.h), "stf_plan_record")
+        nhwc.RECORDING = True
+        try:
+            return fn()
+        finally:
+            nhwc.RECORDING = False
+            _lib.check(self.lib.stf_plan_stop(), "stf_plan_stop")
+            self.n = self.lib.stf_plan_size(self.h)
+
+    def size(self):
+        return self.lib.stf_plan_size(self.h)
+
+    def replay(self, first=0, last=None):
+        last = self.n if last is None else last
+        if last > first:
+            tag = TIMED.encode() if TIMED is not None else None
+            _lib.check(self.lib.stf_plan_replay(self.h, first, last, tag), "stf_plan_replay")
+
+    def timing(self):
+        """(launches, ms, flops) of the TIMED ranges replayed since the last call (syncs)."""
+        n, ms, fl = ctypes.c_int(0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+        _lib.check(self.lib.stf_plan_timing(self.h, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(fl)),
+                   "stf_plan_timing")
+        return n.value, ms.value, fl.value
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            self.lib.stf_plan_destroy(h)
+
+
+def _pool_ctx():
+    """A private memory pool for the recorded step's buffers (a backstop behind
+    ``nhwc.KEEP``: nothing outside the plan can ever be given one of its blocks)."""
+    if os.environ.get("STF_PLAN_POOL", "1") == "0" or not hasattr(torch.cuda, "MemPool"):
+        return None, None
+    pool = torch.cuda.MemPool()
+    return pool, torch.cuda.use_mem_pool(pool)
+
+
+class StepRuntime:
+    """Plan cache of one program (UNetProgram / STFProgram): the training step's forward
+    and backward, recorded at the ``warm``-th step of a signature and replayed after."""
+
+    def __init__(self, prog):
+        self.prog = prog
+        self.warm = int(os.environ.get("STF_PLAN_WARM", "1"))
+        self._reset()
+
+    def _reset(self):
+        self.sig = None
+        self.seen = 0
+        self.fwd = self.bwd = None
+        self.x = self.logits = self.S = None
+        self.bsig = None
+        self.dl = None
+        self.marks = []
+        self.keep = []
+        self.bkeep = []
+        self.pool = None
+        self.owner = None      # weakref to the autograd ctx holding the static S until its backward
+
+    # ------------------------------------------------------------------ signatures
+    def _signature(self, x, training):
+        p = self.prog
+        m = p.m
+        return (tuple(x.shape), x.dtype, x.device, training, _lib.storage_dtype(), _lib.stream(),
+                p.flat.data.data_ptr(), tuple(b.data_ptr() for b in m.buffers()))
+
+    # ------------------------------------------------------------------ forward
+    def busy(self):
+        """The static buffers still belong to an earlier forward whose backward has not run
+        (two forwards before their backwards): a new forward must not overwrite them."""
+        o = self.owner() if self.owner is not None else None
+        return o is not None and self.S is not None and getattr(o, "saved", None) is self.S
+
+    def forward(self, x, training, need_bwd, ctx=None):
+        """The program's forward(x, training, need_bwd) through the plan cache; only the
+        training step (training and need_bwd) is planned, everything else runs eagerly.
+        ``ctx``: the autograd ctx that will hold the returned state until its backward."""
+        p = self.prog
+        if not (enabled() and training and need_bwd and nhwc.TIMER is None) or self.busy():
+            return p.forward(x, training, need_bwd)
+        if ctx is not None:
+            self.owner = weakref.ref(ctx)
+        sig = self._signature(x, training)
+        if sig != self.sig:
+            self._reset()
+            self.sig = sig
+        if self.fwd is None:
+            self.seen += 1
+            if self.seen <= self.warm:
+                return p.forward(x, training, need_bwd)
+            return self._record_forward(x, training)
+        self.x.copy_(x)
+        self.fwd.replay()
+        return self.logits, self.S
+
+    def _record_forward(self, x, training):
+        pool, ctx = _pool_ctx()
+        self.pool = pool
+        keep = self.keep = []
+        nhwc.KEEP = keep
+        try:
+            if ctx is not None:
+                ctx.__enter__()
+            try:
+                self.x = nhwc.empty(tuple(x.shape), x.dtype, x.device)
+                self.x.copy_(x)
+                plan = Plan()
+                logits, S = plan.record(lambda: self.prog.forward(self.x, training, True))
+            finally:
+                if ctx is not None:
+                    ctx.__exit__(None, None, None)
+        finally:
+            nhwc.KEEP = None
+        self.fwd, self.logits, self.S = plan, logits, S
+        return logits, S
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, S, dlogits):
+        p = self.prog
+        if self.fwd is None or S is not self.S or not enabled() or nhwc.TIMER is not None:
+            return p.backward(S, dlogits)
+        bsig = (tuple(dlogits.shape), p.flat.grad.data_ptr(), p.grad_ready_hook is not None, _lib.stream())
+        if self.bwd is None or bsig != self.bsig:
+            return self._record_backward(S, dlogits, bsig)
+        self.dl.copy_(dlogits)
+        pos = 0
+        hook = p.grad_ready_hook
+        for idx, off in self.marks:
+            self.bwd.replay(pos, idx)
+            hook(off)
+            pos = idx
+        self.bwd.replay(pos)
+
+    def _record_backward(self, S, dlogits, bsig):
+        p = self.prog
+        self.bwd = None
+        self.bkeep = []
+        nhwc.KEEP = self.bkeep
+        ctx = torch.cuda.use_mem_pool(self.pool) if self.pool is not None else None
+        plan = Plan()
+        marks = []
+        real_hook = p.grad_ready_hook
+        if real_hook is not None:
+            def hook(off):
+                marks.append((plan.size(), off))
+                real_hook(off)
+            p.grad_ready_hook = hook
+        try:
+            if ctx is not None:
+                ctx.__enter__()
+            try:
+                self.dl = nhwc.empty(tuple(dlogits.shape), dlogits.dtype, dlogits.device)
+                self.dl.copy_(dlogits)
+                plan.record(lambda: p.backward(S, self.dl))
+            finally:
+                if ctx is not None:
+                    ctx.__exit__(None, None, None)
+        finally:
+            nhwc.KEEP = None
+            p.grad_ready_hook = real_hook
+        self.bwd, self.bsig, self.marks = plan, bsig, marks
+
+    def timing(self):
+        """Summed (launches, ms, flops) of the TIMED kernel in this runtime's replays."""
+        tot = [0, 0.0, 0.0]
+        for pl in (self.fwd, self.bwd):
+            if pl is not None:
+                n, ms, fl = pl.timing()
+                tot[0] += n
+                tot[1] += ms
+                tot[2] += fl
+        return tuple(tot)

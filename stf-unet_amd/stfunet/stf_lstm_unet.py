@@ -33,6 +33,7 @@ from . import _lib, nhwc
 from ._lib import LstmEpi, call, stream
 from .flat import FlatParams
 from .nhwc import BNState, Feat, _p, new_feat, rows, zeros_feat
+from .plan import StepRuntime
 
 
 # ------------------------------------------------------------------ module tree
@@ -221,12 +222,12 @@ class LSTMProgram:
         C, dev = self.C, lbuf.buf.device
         L = self.lstm
         npix = B * lbuf.H * lbuf.W
-        wcat = torch.empty(8 * C * C, dtype=nhwc.sdt(), device=dev)
-        wcat_t = torch.empty_like(wcat)
-        bias = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        wcat = nhwc.empty(8 * C * C, nhwc.sdt(), dev)
+        wcat_t = nhwc.empty(8 * C * C, nhwc.sdt(), dev)
+        bias = nhwc.empty(4 * C, torch.float32, dev)
         call("stf_lstm_pack", _p(L.weight_ih_l0.detach()), _p(L.weight_hh_l0.detach()), _p(L.bias_ih_l0.detach()),
              _p(L.bias_hh_l0.detach()), C, _p(wcat), _p(wcat_t), _p(bias), stream())
-        cst = torch.empty(T, npix, C, dtype=torch.float32, device=dev)
+        cst = nhwc.empty((T, npix, C), torch.float32, dev)
         fused = self.fused(lbuf, hT)
         coop = not fused and self.coop(lbuf, hT)
         if fused:
@@ -240,9 +241,9 @@ class LSTMProgram:
             lbuf.check()
             hT.check()
             lib = _lib.load()
-            sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
+            sync = nhwc.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, torch.int32, dev)
             # the activated gates (fp32) are kept for the cooperative backward (no recompute)
-            gates = torch.empty(T, npix, 4 * C, dtype=torch.float32, device=dev) if need_bwd else None
+            gates = nhwc.empty((T, npix, 4 * C), torch.float32, dev) if need_bwd else None
             call("stf_lstm_coop_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs,
                  _p(gates), _p(sync), self.max_wg, stream())
             self.last_sync = (sync, npix, T)
@@ -276,12 +277,12 @@ class LSTMProgram:
             # exchanged in-launch inside each pixel block; the forward's gates, no recompute)
             dhT.check()
             lib = _lib.load()
-            sync = torch.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, dtype=torch.int32, device=dev)
+            sync = nhwc.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, torch.int32, dev)
             call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
                  dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, stream())
             self.last_sync = (sync, npix, T)
         else:
-            dc = torch.empty(npix, C, dtype=torch.float32, device=dev)
+            dc = nhwc.empty((npix, C), torch.float32, dev)
             for t in range(T - 1, -1, -1):
                 dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
                 dgt = rows(dg, t * B, B)
@@ -291,9 +292,9 @@ class LSTMProgram:
                               1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
                 nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
                 nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
-        dwcat = torch.empty(8 * C * C, dtype=torch.float32, device=dev)
+        dwcat = nhwc.empty(8 * C * C, torch.float32, dev)
         nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat, defer=False)
-        dbcat = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        dbcat = nhwc.empty(4 * C, torch.float32, dev)
         nhwc.channel_sum(dg, dbcat)
         call("stf_lstm_unpack_grad", _p(dwcat), _p(dbcat), C, _p(gv(L.weight_ih_l0)), _p(gv(L.weight_hh_l0)),
              _p(gv(L.bias_ih_l0)), _p(gv(L.bias_hh_l0)), stream())
@@ -326,6 +327,15 @@ class STFProgram:
         self.lstm_progs = [LSTMProgram(lstm, side_wg if k < 3 else 0) for k, lstm in enumerate(self.lstms)]
         self._side = None
         self._wstream = None
+        self._ident = {}
+        self.runtime = StepRuntime(self)
+
+    def _identity(self, C, dev):
+        """BatchNorm-identity state of the head's input (no BN there), made once per (C, device)."""
+        key = (C, str(dev), nhwc.sdt())
+        if key not in self._ident:
+            self._ident[key] = BNState.identity(C, dev)
+        return self._ident[key]
 
     def side_streams(self, dev):
         """One HIP stream per LSTM scale 1-3.  The four per-pixel LSTMs are independent
@@ -341,7 +351,7 @@ class STFProgram:
         nhwc.flush_bn_grads()          # grouped BN dgamma/dbeta before the buckets read them
         if self.grad_ready_hook is not None:
             if self._wstream is not None:       # the bucket reads this module's weight gradients
-                torch.cuda.current_stream().wait_stream(self._wstream)
+                nhwc.wait(torch.cuda.current_stream(), self._wstream)
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
@@ -365,7 +375,7 @@ class STFProgram:
         finally:
             nhwc.WGRAD_STREAM = nhwc.WGRAD_MAIN = None
             if ws is not None:
-                torch.cuda.current_stream(dlogits.device).wait_stream(ws)
+                nhwc.wait(torch.cuda.current_stream(dlogits.device), ws)
             nhwc.flush_bn_grads()
             nhwc.ACTIVE_PACKS = None
 
@@ -410,7 +420,7 @@ class STFProgram:
         h4, w4 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
         p0 = new_feat(N, h4, w4, 64, dev)
         # the window argmax the backward routes through (eval-mode backward needs it too)
-        S.pool_arg = torch.empty(N * h4 * w4 * 64, dtype=torch.uint8, device=dev) if need_bwd else None
+        S.pool_arg = nhwc.empty(N * h4 * w4 * 64, torch.uint8, dev) if need_bwd else None
         call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), _p(S.pool_arg), stream())
         S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
         # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat);
@@ -451,7 +461,7 @@ class STFProgram:
                 d = self.decoders[2 - li]
                 Cout = d.up.out_channels
                 dc = dcat[2 - li] = new_feat(B, hh, ww, Cout + d.fusion.in_channels - Cout, dev)
-                side[li].wait_stream(main)
+                nhwc.wait(side[li], main)
                 with torch.cuda.stream(side[li]):
                     S.lstm[li] = lp.forward(lbuf, T, B, dc.slice(dc.C - lp.C, lp.C), need_bwd)
             else:
@@ -462,7 +472,7 @@ class STFProgram:
         S.dec = []
         cur = e4f
         for i, d in enumerate(self.decoders):
-            main.wait_stream(side[2 - i])      # h_T of lstm 2-i fills the skip half of dcat[i]
+            nhwc.wait(main, side[2 - i])       # h_T of lstm 2-i fills the skip half of dcat[i]
             cat = dcat[i]
             Cout = d.up.out_channels
             nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, cat.slice(0, Cout), 3, 3, 2, 1,
@@ -485,8 +495,8 @@ class STFProgram:
         S.fr = self.final_res.forward(u1, fr_out, training, 1)
         S.d2out, S.u1 = cur, u1
         K = m.final.out_channels
-        logits = torch.empty(B, K, u1.H, u1.W, dtype=torch.float32, device=dev)
-        S.ident = BNState.identity(fr_out.C, dev)
+        logits = nhwc.empty((B, K, u1.H, u1.W), torch.float32, dev)
+        S.ident = self._identity(fr_out.C, dev)
         S.head_w = m.final.weight.detach().reshape(K, -1).contiguous()
         call("stf_head_fwd", fr_out.ptr(), B, u1.H, u1.W, fr_out.C, _p(S.ident.scale), _p(S.ident.shift),
              _p(S.head_w), _p(m.final.bias.detach()), K, _p(logits), stream())
@@ -506,8 +516,8 @@ class STFProgram:
         lib = _lib.load()
         tiles = lib.stf_head_tiles(B, fr_out.H, fr_out.W, C)
         g = new_feat(B, fr_out.H, fr_out.W, C, dev)
-        bnp = torch.empty(tiles * 2 * C, dtype=torch.float32, device=dev)
-        hp = torch.empty((tiles + 1) * K * (C + 1), dtype=torch.float32, device=dev)
+        bnp = nhwc.empty(tiles * 2 * C, torch.float32, dev)
+        hp = nhwc.empty((tiles + 1) * K * (C + 1), torch.float32, dev)
         call("stf_head_bwd", _p(dlogits), fr_out.ptr(), B, fr_out.H, fr_out.W, C, _p(S.ident.scale),
              _p(S.ident.shift), _p(S.ident.mean), _p(S.ident.invstd), _p(S.head_w), K, g.ptr(), _p(bnp), _p(hp),
              _p(gv(m.final.weight)), _p(gv(m.final.bias)), stream())
@@ -547,7 +557,7 @@ class STFProgram:
             nhwc.igemm(dup, nhwc.pack_weight(d.up.weight, 3), dsv.x.C, dx, 3, 3, 2, 1)
             k = 2 - i                                          # skip of scale k (decoder4 -> idx 2)
             dhT[k] = dcat.slice(Cout, dcat.C - Cout)
-            side[k].wait_stream(main)
+            nhwc.wait(side[k], main)
             with torch.cuda.stream(side[k]):
                 lstm_bwd(k)
             dcur = dx
@@ -560,7 +570,7 @@ class STFProgram:
         eager = self.grad_ready_hook is not None or P
         for k in (3, 2, 1, 0):
             if eager and k < 3:
-                main.wait_stream(side[k])
+                nhwc.wait(main, side[k])
             self._done(self.lstms[k])
         if P:
             for k in (3, 2, 1, 0):
@@ -570,7 +580,7 @@ class STFProgram:
         for li in (3, 2, 1, 0):
             progs, saved = self.layers[li], S.enc[li]
             if li < 3:
-                main.wait_stream(side[li])
+                nhwc.wait(main, side[li])
             dout = de[li]
             for bi in range(len(progs) - 1, -1, -1):
                 bp, s = progs[bi], saved[bi]
@@ -587,27 +597,28 @@ class STFProgram:
         w1 = m.conv1.weight
         kreal = w1[0].numel()
         if S.stem_gather:                      # 8-channel packed input, 7x7/s2 gather
-            tmp = torch.empty(w1.shape[0] * 8 * 49, dtype=torch.float32, device=dev)
+            tmp = nhwc.empty(w1.shape[0] * 8 * 49, torch.float32, dev)
             nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp, defer=False)
-            gv(w1).copy_(tmp.view(w1.shape[0], 8, 7, 7)[:, :w1.shape[1]])
+            nhwc.copy_rows(tmp, 8 * 49, gv(w1), w1.shape[1] * 49, w1.shape[0], w1.shape[1] * 49)
         elif S.xin.C == kreal:
             nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, gv(w1))
         else:
-            tmp = torch.empty(w1.shape[0] * S.xin.C, dtype=torch.float32, device=dev)
+            tmp = nhwc.empty(w1.shape[0] * S.xin.C, torch.float32, dev)
             nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, tmp, defer=False)
-            gv(w1).copy_(tmp.view(w1.shape[0], S.xin.C)[:, :kreal].view(w1.shape))
+            nhwc.copy_rows(tmp, S.xin.C, gv(w1), kreal, w1.shape[0], kreal)
 
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
         fus = getattr(self.m, f"pk_fusion{k + 1}")
         pkb = S.pkbuf[k]
         C = de.C
-        tmp = torch.empty(C * pkb.C, dtype=torch.float32, device=de.buf.device)
+        tmp = nhwc.empty(C * pkb.C, torch.float32, de.buf.device)
         nhwc.wgrad(de, pkb, 1, 1, 1, 0, tmp, defer=False)
-        gv(fus.weight).copy_(tmp.view(C, pkb.C, 1, 1)[:, :fus.in_channels])
+        cin = fus.in_channels
+        nhwc.copy_rows(tmp, pkb.C, gv(fus.weight), cin, C, cin)
         nhwc.channel_sum(de, gv(fus.bias))
         dpk = new_feat(pkb.N, pkb.H, pkb.W, pkb.C, de.buf.device)
-        w = torch.zeros(C, pkb.C, 1, 1, dtype=torch.float32, device=de.buf.device)
-        w[:, :fus.in_channels].copy_(fus.weight.detach())
+        w = nhwc.memset0(nhwc.empty((C, pkb.C, 1, 1), torch.float32, de.buf.device))
+        nhwc.copy_rows(fus.weight.detach(), cin, w, pkb.C, C, cin)
         nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0)
         return dpk.slice(0, C)
 
@@ -620,10 +631,10 @@ class _STFFunction(torch.autograd.Function):
                                       "sequence must not require grad")
         need_bwd = any(ctx.needs_input_grad[3:])
         with _lib.storage(storage):
-            logits, saved = prog.forward(x, prog.m.training, need_bwd)
+            logits, saved = prog.runtime.forward(x, prog.m.training, need_bwd, ctx)
         ctx.storage = storage
         ctx.prog, ctx.saved = prog, saved
-        return logits
+        return logits.detach()        # the plan's static logits: a fresh tensor object per step
 
     @staticmethod
     def backward(ctx, dlogits):
@@ -631,7 +642,7 @@ class _STFFunction(torch.autograd.Function):
         dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
         with _lib.storage(ctx.storage):
-            prog.backward(ctx.saved, dlogits)
+            prog.runtime.backward(ctx.saved, dlogits)
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0)

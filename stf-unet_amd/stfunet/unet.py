@@ -29,6 +29,7 @@ import torch.nn as nn
 from . import _lib, nhwc
 from .flat import FlatParams
 from .nhwc import Feat, new_feat
+from .plan import StepRuntime
 
 
 def _double_conv(cin, cout):
@@ -108,9 +109,9 @@ class DoubleConvProgram:
         if src.C == cin:
             nhwc.wgrad(dy1, src, 3, 3, 1, 1, out)
         else:   # zero-padded input channels (in_channels % 8 != 0): drop the padded columns
-            tmp = torch.empty(self.cout * src.C * 9, dtype=torch.float32, device=out.device)
+            tmp = nhwc.empty(self.cout * src.C * 9, torch.float32, out.device)
             nhwc.wgrad(dy1, src, 3, 3, 1, 1, tmp, defer=False)
-            out.copy_(tmp.view(self.cout, src.C, 3, 3)[:, :cin])
+            nhwc.copy_rows(tmp, src.C * 9, out, cin * 9, self.cout, cin * 9)
 
 
 class UNetProgram:
@@ -131,11 +132,12 @@ class UNetProgram:
         # set by _UNetFunction for the backward in flight: also return d(loss)/d(input)
         self.want_dx = False
         self.dx = None
+        self.runtime = StepRuntime(self)
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
             if nhwc.WGRAD_STREAM is not None:   # the bucket reads this module's weight gradients
-                torch.cuda.current_stream().wait_stream(nhwc.WGRAD_STREAM)
+                nhwc.wait(torch.cuda.current_stream(), nhwc.WGRAD_STREAM)
             first = next(module.parameters())
             self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
 
@@ -162,7 +164,7 @@ class UNetProgram:
         finally:
             nhwc.WGRAD_STREAM = nhwc.WGRAD_MAIN = None
             if ws is not None:
-                torch.cuda.current_stream(dlogits.device).wait_stream(ws)
+                nhwc.wait(torch.cuda.current_stream(dlogits.device), ws)
             nhwc.ACTIVE_PACKS = None
 
     def _forward(self, x, training, need_bwd):
@@ -205,7 +207,7 @@ class UNetProgram:
         # OutConv fused with dec1's last BN+ReLU
         s = S.dec[-1]
         K = m.out_conv.out_channels
-        logits = torch.empty(N, K, H, W, dtype=torch.float32, device=dev)
+        logits = nhwc.empty((N, K, H, W), torch.float32, dev)
         S.head_w = m.out_conv.weight.detach().reshape(K, -1).contiguous()
         nhwc.call("stf_head_fwd", s.y2.ptr(), N, H, W, s.y2.C, nhwc._p(s.bn2.scale), nhwc._p(s.bn2.shift),
                   nhwc._p(S.head_w), nhwc._p(m.out_conv.bias.detach()), K, nhwc._p(logits), nhwc.stream())
@@ -227,8 +229,8 @@ class UNetProgram:
         lib = nhwc._lib.load()
         tiles = lib.stf_head_tiles(N, H, W, C)
         g = new_feat(N, H, W, C, dev)
-        bnp = torch.empty(tiles * 2 * C, dtype=torch.float32, device=dev)
-        hp = torch.empty((tiles + 1) * K * (C + 1), dtype=torch.float32, device=dev)
+        bnp = nhwc.empty(tiles * 2 * C, torch.float32, dev)
+        hp = nhwc.empty((tiles + 1) * K * (C + 1), torch.float32, dev)
         nhwc.call("stf_head_bwd", nhwc._p(dlogits), s.y2.ptr(), N, H, W, C, nhwc._p(s.bn2.scale),
                   nhwc._p(s.bn2.shift), nhwc._p(s.bn2.mean), nhwc._p(s.bn2.invstd), nhwc._p(S.head_w), K,
                   g.ptr(), nhwc._p(bnp), nhwc._p(hp), nhwc._p(gv(m.out_conv.weight)),
@@ -279,11 +281,14 @@ class _UNetFunction(torch.autograd.Function):
                                       "channel-padded then)")
         need_bwd = any(ctx.needs_input_grad[3:]) or ctx.need_dx
         with _lib.storage(storage):
-            logits, saved = prog.forward(x, prog.m.training, need_bwd)
+            if ctx.need_dx:
+                logits, saved = prog.forward(x, prog.m.training, need_bwd)
+            else:
+                logits, saved = prog.runtime.forward(x, prog.m.training, need_bwd, ctx)
         ctx.storage = storage
         ctx.prog = prog
         ctx.saved = saved
-        return logits
+        return logits.detach()        # the plan's static logits: a fresh tensor object per step
 
     @staticmethod
     def backward(ctx, dlogits):
@@ -293,7 +298,7 @@ class _UNetFunction(torch.autograd.Function):
         prog.want_dx, prog.dx = ctx.need_dx, None
         try:
             with _lib.storage(ctx.storage):
-                prog.backward(ctx.saved, dlogits)
+                prog.runtime.backward(ctx.saved, dlogits)
         finally:
             prog.want_dx = False
         ctx.saved = None
