@@ -24,6 +24,7 @@ struct WArgs {
   const uint16_t* dy; const uint16_t* x; float* ws;
   int N, Hs, Ws, Cs, xcs, Hd, Wd, R, S, st, pad, M, Nout, dycs, chunk;
   int colmajor;         // fused 3x3: walk pixel tiles column-major (vertical neighbours in turn)
+  int one_slab;         // timing-only ablation (STF_WGRAD_ONE_SLAB=1): every split writes slab 0
 };
 
 template <int BM, int BN, int BKP, bool GENERAL>
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   }
 
   const int RSC = 9 * a.Cs;
-  float* out = a.ws + (size_t)split * a.Nout * RSC;
+  float* out = a.ws + (size_t)(a.one_slab ? 0 : split) * a.Nout * RSC;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_dma_kernel(WArgs a, int tiles_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (dummy) DMAs
 
   const int RSC = 9 * a.Cs;
-  float* out = a.ws + (size_t)split * a.Nout * RSC;
+  float* out = a.ws + (size_t)(a.one_slab ? 0 : split) * a.Nout * RSC;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -771,6 +772,10 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.dycs = a->dy_cstride; w.chunk = chunk;
   static const int colmajor = [] { const char* e = getenv("STF_WGRAD_COLMAJOR"); return e ? atoi(e) : 1; }();
   w.colmajor = colmajor;
+  // timing-only ablation: the split-K slabs of the fused 3x3 kernel all land in slab 0 (L2-resident:
+  // no slab traffic to HBM; the sums are wrong) -- the upper bound of folding the slabs in-kernel
+  static const int one_slab = [] { const char* e = getenv("STF_WGRAD_ONE_SLAB"); return e && e[0] == '1'; }();
+  w.one_slab = one_slab;
   hipStream_t s = (hipStream_t)stream;
   const int rsc = c.R * c.S * c.Cs;
   if (const int pw = fused_pw(a)) {

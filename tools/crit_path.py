@@ -16,7 +16,13 @@ rows.sort()
 short = lambda n: (n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0])[:70]
 spins = [i for i, r in enumerate(rows) if "spin" in r[3].lower() or "sleep" in r[3].lower()]
 if not spins:
-    sys.exit("no spin kernel found")
+    # plan-replayed steps (no spin kernel needed: the host is ahead): a step = from the end
+    # of one optimizer kernel to the end of the next
+    spins = [i for i, r in enumerate(rows) if "adamw" in r[3]]
+    rows = rows[:spins[-1] + 1]     # the last full step ends with the last optimizer kernel
+    spins = spins[:-1]
+if not spins:
+    sys.exit("no spin / optimizer kernel found")
 steps = []
 for k, i in enumerate(spins):
     j = spins[k + 1] if k + 1 < len(spins) else len(rows)
