@@ -512,7 +512,225 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* 
   }
 }
 
+// ------------------------------------------------------------------ group-major streaming passes
+// The same three element-wise passes with the grid split by statistics group (blockIdx.y = g):
+// a thread's channel chunk and its group's affine / coefficient vectors are fixed, so the loop
+// carries no per-unit division (the kernels above divide 64-bit unit and pixel indices by C/8
+// and by the group size for every 16-B unit), and every thread issues the loads of UPT units
+// (a block covers UPT x 256 consecutive units per iteration)
+// before it uses any (UPT x 2-3 16-B loads in flight per lane: the STF encoder's 8-67 MB tensors
+// are latency-bound at one unit per iteration).  Index math is 32-bit: units per group < 2^31
+// (checked by the launchers).  Unit u of group g: pixel g * Mg + (u >> cgs), chunk u & (CG - 1).
+constexpr int UPT = 4;
+
+template <bool RES>
+__global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift, int relu, int res_mode,
+                                                      const uint16_t* __restrict__ res, int rcs,
+                                                      const float* __restrict__ rscale,
+                                                      const float* __restrict__ rshift, uint16_t* __restrict__ out,
+                                                      int ocs) {
+  const int g = blockIdx.y, C = 8 << cgs;
+  const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
+  const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
+  const int cg = threadIdx.x & ((1 << cgs) - 1);
+  float sc[8], sh[8], rs[8], rh[8];
+  load_affine(scale + (size_t)g * C, cg * 8, sc);
+  load_affine(shift + (size_t)g * C, cg * 8, sh);
+  if (RES && res_mode == 2) {
+    load_affine(rscale + (size_t)g * C, cg * 8, rs);
+    load_affine(rshift + (size_t)g * C, cg * 8, rh);
+  }
+  const size_t p0 = (size_t)g * Mg;
+  for (int u = u0; u < upg; u += S) {
+    uint4 yv[UPT], rv[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk < upg) {
+        const size_t p = p0 + (uk >> cgs);
+        yv[k] = *reinterpret_cast<const uint4*>(y + p * ycs + cg * 8);
+        if (RES) rv[k] = *reinterpret_cast<const uint4*>(res + p * rcs + cg * 8);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk >= upg) break;
+      float v[8];
+      unpack8(yv[k], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+      if (RES) {
+        float r[8];
+        unpack8(rv[k], r);
+        if (res_mode == 2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) r[j] = r[j] * rs[j] + rh[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += r[j];
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      *reinterpret_cast<uint4*>(out + (p0 + (uk >> cgs)) * ocs + cg * 8) = pack8(v);
+    }
+  }
+}
+
+// mask_mode 0: none, 1: relu(y*scale+shift) > 0, 2: mask_src > 0; same sums as bn_bwd_reduce_kernel
+template <int MASK>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_g_kernel(const uint16_t* __restrict__ dz, int dzcs,
+                                                             const uint16_t* __restrict__ y, int ycs, int Mg,
+                                                             int cgs, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const uint16_t* __restrict__ msrc, int mcs,
+                                                             uint16_t* __restrict__ g_out, float* __restrict__ partial) {
+  __shared__ float red[NT][17];
+  const int g = blockIdx.y, CG = 1 << cgs, C = 8 << cgs;
+  const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
+  const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
+  const int cg = threadIdx.x & (CG - 1);
+  float sc[8], sh[8], mu[8], is[8];
+  if (MASK == 1) {
+    load_affine(scale + (size_t)g * C, cg * 8, sc);
+    load_affine(shift + (size_t)g * C, cg * 8, sh);
+  }
+  load_affine(mean + (size_t)g * C, cg * 8, mu);
+  load_affine(invstd + (size_t)g * C, cg * 8, is);
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const size_t p0 = (size_t)g * Mg;
+  for (int u = u0; u < upg; u += S) {
+    uint4 yv[UPT], zv[UPT], mv[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk < upg) {
+        const size_t p = p0 + (uk >> cgs);
+        yv[k] = *reinterpret_cast<const uint4*>(y + p * ycs + cg * 8);
+        zv[k] = *reinterpret_cast<const uint4*>(dz + p * dzcs + cg * 8);
+        if (MASK == 2) mv[k] = *reinterpret_cast<const uint4*>(msrc + p * mcs + cg * 8);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk >= upg) break;
+      float v[8], d[8], mk[8];
+      unpack8(yv[k], v);
+      unpack8(zv[k], d);
+      if (MASK == 2) unpack8(mv[k], mk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bool keep = true;
+        if (MASK == 1) keep = v[j] * sc[j] + sh[j] > 0.f;
+        else if (MASK == 2) keep = mk[j] > 0.f;
+        const float gj = keep ? d[j] : 0.f;
+        d[j] = gj;
+        sg[j] += gj;
+        sgx[j] += gj * (v[j] - mu[j]) * is[j];
+      }
+      if (g_out) *reinterpret_cast<uint4*>(g_out + (p0 + (uk >> cgs)) * C + cg * 8) = pack8(d);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
+  __syncthreads();
+  const size_t row = (size_t)g * gridDim.x + blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int gg = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int t = gg; t < NT; t += CG) { a += red[t][j]; b += red[t][8 + j]; }
+    partial[row * 2 * C + c] = a;
+    partial[row * 2 * C + C + c] = b;
+  }
+}
+
+// dy = A*g' + B*y + C (as bn_bwd_apply_kernel); bias_partial rows = g * gridDim.x + blockIdx.x
+template <bool MASK>
+__global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in, int gcs,
+                                                            const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
+                                                            const float* __restrict__ coef,
+                                                            const float* __restrict__ mscale,
+                                                            const float* __restrict__ mshift, uint16_t* dy,
+                                                            int dycs, float* __restrict__ bias_partial) {
+  __shared__ float red[NT][9];
+  const int g = blockIdx.y, CG = 1 << cgs, C = 8 << cgs;
+  const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
+  const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
+  const int cg = threadIdx.x & (CG - 1);
+  float A[8], B[8], Cc[8], ms[8], mh[8];
+  load_affine(coef + (size_t)g * 3 * C, cg * 8, A);
+  load_affine(coef + (size_t)g * 3 * C + C, cg * 8, B);
+  load_affine(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
+  if (MASK) {
+    load_affine(mscale + (size_t)g * C, cg * 8, ms);
+    load_affine(mshift + (size_t)g * C, cg * 8, mh);
+  }
+  float sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const size_t p0 = (size_t)g * Mg;
+  for (int u = u0; u < upg; u += S) {
+    uint4 gq[UPT], yq[UPT];
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk < upg) {
+        const size_t p = p0 + (uk >> cgs);
+        gq[k] = *reinterpret_cast<const uint4*>(g_in + p * gcs + cg * 8);
+        yq[k] = *reinterpret_cast<const uint4*>(y + p * ycs + cg * 8);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int uk = u + k * NT;
+      if (uk >= upg) break;
+      float gv[8], yv[8];
+      unpack8(gq[k], gv);
+      unpack8(yq[k], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gj = (MASK && !(yv[j] * ms[j] + mh[j] > 0.f)) ? 0.f : gv[j];
+        gv[j] = A[j] * gj + B[j] * yv[j] + Cc[j];
+        sb[j] += gv[j];
+      }
+      *reinterpret_cast<uint4*>(dy + (p0 + (uk >> cgs)) * dycs + cg * 8) = pack8(gv);
+    }
+  }
+  if (!bias_partial) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = sb[j];
+  __syncthreads();
+  const size_t row = (size_t)g * gridDim.x + blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int gg = c >> 3, j = c & 7;
+    float a = 0.f;
+    for (int t = gg; t < NT; t += CG) a += red[t][j];
+    bias_partial[row * C + c] = a;
+  }
+}
+
 }  // namespace
+
+// the group-major kernels (STF_BN_G=0: the per-unit-division kernels, A/B); usable when C / 8 is
+// a power of two dividing the block and a group's units fit 32-bit indices
+static bool bn_g_ok(long Mg, int C) {
+  static const bool on = [] { const char* e = getenv("STF_BN_G"); return !(e && e[0] == '0'); }();
+  const int CG = C / 8;
+  return on && C % 8 == 0 && CG > 0 && (CG & (CG - 1)) == 0 && NT % CG == 0 && Mg * CG < (1L << 31);
+}
+static int log2i(int v) { return 31 - __builtin_clz(v); }
+// blocks per group: about UPT units per thread, at least one, the whole grid <= cap blocks
+static int g_tiles(long upg, int groups, long cap) {
+  long t = (upg + (long)NT * UPT - 1) / ((long)NT * UPT);
+  const long per = cap / groups > 0 ? cap / groups : 1;
+  if (t > per) t = per;
+  return (int)(t < 1 ? 1 : t);
+}
 
 // sum over tiles of partial[t][C] -> out[C] (fixed order); shared with misc.hip / loss.hip
 // launch: grid ceil(C/16), 256 threads (16 channels x 16 row-lanes)
@@ -561,6 +779,20 @@ extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int
   if (blocks < 1) return 0;
   hipStream_t s = (hipStream_t)stream;
   const long Mg = M / groups;
+  if (!pooled && bn_g_ok(Mg, C)) {
+    const int cgs = log2i(C / 8);
+    const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
+    if (res)
+      hipLaunchKernelGGL(bn_act_g_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg, cgs,
+                         scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale, res_shift,
+                         (uint16_t*)out, out_cstride);
+    else
+      hipLaunchKernelGGL(bn_act_g_kernel<false>, grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg, cgs,
+                         scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
+                         (const float*)nullptr, (uint16_t*)out, out_cstride);
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
   if (pooled)
     hipLaunchKernelGGL(bn_act_kernel<true>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (long)N, H,
                        W, C, Mg, scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
@@ -591,6 +823,20 @@ extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpo
   const int tpg = stf_bn_bwd_tiles(N, H, W, C, groups, dpool != nullptr);
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(tpg * groups);
+  const long Mgp = (long)N * H * W / groups;
+  if (!dpool && bn_g_ok(Mgp, C)) {
+    const dim3 g2(tpg, groups);
+    const int cgs = log2i(C / 8);
+#define STF_RG(MM) hipLaunchKernelGGL(bn_bwd_reduce_g_kernel<MM>, g2, dim3(NT), 0, s, (const uint16_t*)dz, dz_cstride, \
+                                      (const uint16_t*)y, y_cstride, (int)Mgp, cgs, scale, shift, mean, invstd,     \
+                                      (const uint16_t*)mask_src, mask_cstride, (uint16_t*)g_out, partial)
+    if (mask_mode == 1) STF_RG(1);
+    else if (mask_mode == 2) STF_RG(2);
+    else STF_RG(0);
+#undef STF_RG
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
   static const bool lanes = [] { const char* e = getenv("STF_POOL_LANES"); return !(e && e[0] == '0'); }();
   if (dpool && lanes && 64 % (C / 8) == 0 && mask_mode != 2 && (long)N * H * W < (1L << 31))
     hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, grid, dim3(PNT), 0, s, (const uint16_t*)dz, dz_cstride,
@@ -667,11 +913,28 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
                                 void* dy, int dy_cstride, float* bias_partial, float* dbias, stf_stream_t stream) {
   if (!cg_ok(C) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8 || groups < 1 || M % groups) return STF_EINVAL;
   if ((mask_scale == nullptr) != (mask_shift == nullptr)) return STF_EINVAL;
-  const int tiles = stf_bn_bwd_apply_tiles(M, C);
+  int tiles = stf_bn_bwd_apply_tiles(M, C);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
-                     (const uint16_t*)y, y_cstride, (long)M, C, (long)(M / groups), coef, mask_scale, mask_shift,
-                     (uint16_t*)dy, dy_cstride, bias_partial);
+  const long Mg = M / groups;
+  if (bn_g_ok(Mg, C)) {
+    // bias_partial rows: groups x tpg <= stf_bn_bwd_apply_tiles (the caller's allocation)
+    const int tpg = g_tiles(Mg * (C / 8), groups, bias_partial ? tiles : 8192);
+    const dim3 grid(tpg, groups);
+    const int cgs = log2i(C / 8);
+    if (mask_scale)
+      hipLaunchKernelGGL(bn_bwd_apply_g_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                         (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
+                         dy_cstride, bias_partial);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_g_kernel<false>, grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                         (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
+                         dy_cstride, bias_partial);
+    tiles = tpg * groups;
+  } else {
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                       (const uint16_t*)y, y_cstride, (long)M, C, (long)(M / groups), coef, mask_scale, mask_shift,
+                       (uint16_t*)dy, dy_cstride, bias_partial);
+  }
   STF_CHECK_LAUNCH();
   if (bias_partial && dbias) {
     const int S = stf::colsum_stage1(bias_partial, tiles, C, s, 1, stf::FOLD16_ROWS);

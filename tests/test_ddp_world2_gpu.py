@@ -11,7 +11,10 @@ grad_ready_hook, finish() before AdamW).  For UNet and STFLSTMUNet (SURVEY.md 8(
   recomputes both local gradients itself, the kernels being deterministic;
 * buckets went out while the backward ran (more than one per step);
 * after AdamW the parameters are identical on both ranks (all-gathered and compared),
-  while the BatchNorm running statistics differ (per-rank BN, like torch DDP).
+  while the BatchNorm running statistics differ (per-rank BN, like torch DDP);
+* four DDP steps on native plans (stfunet/plan.py: the second step records, the rest replay
+  with the hook running between backward segments) end with exactly the parameters and
+  losses of four eager DDP steps (STF_PLAN=0), and the same on both ranks.
 """
 import os
 import socket
@@ -56,6 +59,42 @@ def _local_grad(which, batch):
     return model.program.flat.grad.detach().clone()
 
 
+def _ddp_steps(which, rank, batches, steps, plan_on):
+    from stfunet import engine
+    from stfunet.ddp import GradAllReduce
+    from stfunet.optim import AdamW
+    os.environ["STF_PLAN"] = "1" if plan_on else "0"
+    try:
+        model = _make(which)
+        opt = AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+        ddp = GradAllReduce(model, bucket_mb=0.5)
+        losses = []
+        for i in range(steps):
+            x, t = batches[(rank + i) % len(batches)]
+            loss = engine.criterion(model(x), t)
+            opt.zero_grad()
+            loss.backward()
+            ddp.finish()
+            opt.step()
+            losses.append(loss.detach().clone())
+        torch.cuda.synchronize()
+        model.program.grad_ready_hook = None
+        return (torch.stack(losses), model.program.flat.data.detach().clone(),
+                model.program.runtime.bwd is not None)
+    finally:
+        os.environ.pop("STF_PLAN", None)
+
+
+def _plan_steps(which, rank, world, batches):
+    le, pe, _ = _ddp_steps(which, rank, batches, 4, False)
+    lp, pp, replayed = _ddp_steps(which, rank, batches, 4, True)
+    ps = [torch.empty_like(pp) for _ in range(world)]
+    dist.all_gather(ps, pp)
+    return dict(plan_replayed=replayed, plan_losses_equal=bool(torch.equal(le, lp)),
+                plan_params_equal=bool(torch.equal(pe, pp)),
+                plan_params_equal_ranks=all(torch.equal(ps[0], o) for o in ps[1:]))
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -94,6 +133,7 @@ def _worker(rank, world, port, q):
                               params_equal=all(torch.equal(ps[0], o) for o in ps[1:]),
                               running_stats_differ=not torch.equal(rms[0], rms[1]),
                               loss=float(loss))
+            res[which].update(_plan_steps(which, rank, world, batches))
     except Exception as e:  # report, do not hang the peer
         res["error"] = repr(e)
     q.put((rank, res))
@@ -121,4 +161,6 @@ def test_grad_allreduce_world2_real_programs():
             assert r["launched"] > 1, (rank, which, r)
             assert r["params_equal"], (rank, which, r)
             assert r["running_stats_differ"], (rank, which, r)
+            assert r["plan_replayed"] and r["plan_losses_equal"] and r["plan_params_equal"], (rank, which, r)
+            assert r["plan_params_equal_ranks"], (rank, which, r)
     assert out[0]["unet"]["loss"] != out[1]["unet"]["loss"]      # the ranks really had different batches

@@ -424,8 +424,12 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
 def test_stf_model_with_cooperative_lstms_matches_per_step(monkeypatch):
     """The whole STF training step with every LSTM on the cooperative kernels (forward and
     backward, STF_LSTM_COOP=1, STF_LSTM_COOP_BWD=1) against the same step on the per-step
-    launches: logits and loss bit for bit (the forward is), every parameter gradient within
-    rel 1e-2 (the per-step dgates x W GEMMs split over K at these small sizes)."""
+    launches: logits and loss bit for bit (the forward is); the decoder's gradients bit for bit
+    (its backward runs before any LSTM's); the LSTMs' within rel 1e-2 (the per-step dgates x W
+    GEMMs split over K at these small sizes); the encoder's -- downstream of the LSTMs' d x_t,
+    through 36 train-mode BatchNorms at initialisation, which amplify any perturbation (DESIGN.md
+    section 4: the fp32 oracle's gradients move 2.3 % for a 1e-6 input change) -- within rel 5e-2,
+    median over them 1e-2."""
     from oracle.init import canonical_state_dict
     from stfunet import STFLSTMUNet
     from stfunet.loss import criterion
@@ -443,8 +447,17 @@ def test_stf_model_with_cooperative_lstms_matches_per_step(monkeypatch):
         loss.backward()
         res[mode] = (out.detach(), loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
     assert torch.equal(res["0"][0], res["1"][0]) and res["0"][1] == res["1"][1]
+    enc = []
     for k, g0 in res["0"][2].items():
-        assert rel(res["1"][2][k], g0) < 1e-2, k
+        e = rel(res["1"][2][k], g0)
+        if k.startswith(("decoder", "upconv1", "final")):
+            assert torch.equal(res["1"][2][k], g0), k
+        elif k.startswith("lstm"):
+            assert e < 1e-2, (k, e)
+        else:
+            assert e < 5e-2, (k, e)
+            enc.append(e)
+    assert float(np.median(enc)) < 1e-2, np.median(enc)
 
 
 def test_stf_eval_mode_backward_vs_oracle():
