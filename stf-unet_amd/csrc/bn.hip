@@ -58,8 +58,8 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __rest
   double mu = 0.0, var = 1.0;
   float* base = stats ? stats + (size_t)g * T * 2 * C : nullptr;
   if (stats) {
-    const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
-    const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
+    double s1, s2;
+    stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
     mu = s1 / Mg;
     var = s2 / Mg - mu * mu;
     if (var < 0) var = 0;
@@ -392,8 +392,8 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __
   const int c = blockIdx.x * 16 + (threadIdx.x & 15);
   const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
   float* base = partial + (size_t)g * T * 2 * C;
-  const double s1 = stf::fold16_finish(stf::fold16_partial(base, S, 2L * C, c, cok), red);
-  const double s2 = stf::fold16_finish(stf::fold16_partial(base + C, S, 2L * C, c, cok), red);
+  double s1, s2;
+  stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
   if (!lead) return;
   const double is = invstd[g * C + c];
   const double A = (double)gamma[c] * is;

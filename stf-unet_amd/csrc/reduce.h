@@ -74,6 +74,46 @@ STF_DEV double fold16_finish(double v, double* red) {
   return tot;
 }
 
+// Both halves of a [rows][2][C] statistics slab at once (the BatchNorm finalize kernels: sum and
+// sum of squares, or sum g and sum g*xhat): every lane issues the loads of both before adding,
+// the four row-lanes a wave holds per column fold by shuffles, and the cross-wave fold is a
+// 16-long chain per column instead of 64 (FOLD_NT / 16 row-lanes).  Fixed order: deterministic.
+// Returns (on threads 0..15) the two totals; ``red`` holds 2 * (blockDim / 64) * 16 doubles.
+STF_DEV void fold16_pair(const float* base, int S, long stride, long off2, long c, bool cok, double* red,
+                         double& o1, double& o2) {
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  if (cok) {
+    const int RL = blockDim.x >> 4;
+    int t = threadIdx.x >> 4;
+    for (; t + RL < S; t += 2 * RL) {
+      const float x0 = base[(long)t * stride + c], y0 = base[(long)t * stride + off2 + c];
+      const float x1 = base[(long)(t + RL) * stride + c], y1 = base[(long)(t + RL) * stride + off2 + c];
+      a0 += x0; b0 += y0; a1 += x1; b1 += y1;
+    }
+    for (; t < S; t += RL) {
+      a0 += base[(long)t * stride + c];
+      b0 += base[(long)t * stride + off2 + c];
+    }
+  }
+  double v1 = a0 + a1, v2 = b0 + b1;
+  v1 += __shfl_xor(v1, 16, 64);
+  v2 += __shfl_xor(v2, 16, 64);
+  v1 += __shfl_xor(v1, 32, 64);
+  v2 += __shfl_xor(v2, 32, 64);
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 16) {
+    red[wave * 16 + lane] = v1;
+    red[(nw + wave) * 16 + lane] = v2;
+  }
+  __syncthreads();
+  o1 = o2 = 0.0;
+  if (threadIdx.x < 16)
+    for (int w = 0; w < nw; ++w) {
+      o1 += red[w * 16 + threadIdx.x];
+      o2 += red[(nw + w) * 16 + threadIdx.x];
+    }
+}
+
 constexpr int FOLD_NT = 1024;         // block size of the fold16 consumers (finalize kernels)
 
 constexpr long FOLD16_ROWS = 1024;    // finalize kernels read up to this many rows directly

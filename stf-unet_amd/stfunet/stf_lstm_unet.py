@@ -281,6 +281,17 @@ class LSTMProgram:
             call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
                  dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, stream())
             self.last_sync = (sync, npix, T)
+        elif st.gates is not None and os.environ.get("STF_LSTM_GATES", "1") != "0":
+            # the cooperative forward kept the activated gates: per step only the cell backward
+            # (elementwise, the same lstm_cell_bwd arithmetic as the recompute epilogue below, so
+            # the same dgates bit for bit) and the [dx | dh] GEMM -- no gate recompute GEMM
+            dc = nhwc.empty((npix, C), torch.float32, dev)
+            for t in range(T - 1, -1, -1):
+                dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
+                dgt = rows(dg, t * B, B)
+                call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None,
+                     dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
+                nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
         else:
             dc = nhwc.empty((npix, C), torch.float32, dev)
             for t in range(T - 1, -1, -1):

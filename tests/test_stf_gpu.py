@@ -386,7 +386,9 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
     backward (stf_lstm_coop_bwd: the forward's gates, dgates and [dx | dh] exchanged in-launch)
     gives the per-step backward's input and weight gradients: bit for bit where the per-step
     dgates x W GEMM runs unsplit (lstm2 at cfg3), else within rel 2e-3 (small pixel counts split
-    that GEMM over K: a different fp32 summation order before the 16-bit rounding)."""
+    that GEMM over K: a different fp32 summation order before the 16-bit rounding).  Mode "g":
+    cooperative forward, per-step backward from the forward's stored gates (cell backward +
+    [dx | dh] GEMM, no gate recompute): bit for bit the per-step path everywhere."""
     from stfunet import nhwc
     from stfunet.stf_lstm_unet import LSTMProgram
     lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
@@ -396,20 +398,22 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
     dhT.buf.normal_()
     prog = LSTMProgram(lstm)
     out = {}
-    monkeypatch.setenv("STF_LSTM_COOP_BWD", "1")
-    for mode in ("0", "1"):
-        monkeypatch.setenv("STF_LSTM_COOP", mode)
+    for mode in ("0", "1", "g"):
+        monkeypatch.setenv("STF_LSTM_COOP", "0" if mode == "0" else "1")
+        monkeypatch.setenv("STF_LSTM_COOP_BWD", "1" if mode == "1" else "0")
         lb = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
         lb.buf.copy_(lbuf.buf)
         hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
         st = prog.forward(lb, T, B, hT)
-        if mode == "1":
-            assert st.coop and prog.coop_error() == 0
+        if mode != "0":
+            assert (st.coop == (mode == "1")) and st.gates is not None and prog.coop_error() == 0
         gv = _Grads(lstm)
         dx = prog.backward(st, dhT, gv)
         if mode == "1":
             assert prog.coop_error() == 0
         out[mode] = [hT.dense(), st.c, lb.buf.clone(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
+    for i, (a, b) in enumerate(zip(out["0"], out["g"])):
+        assert torch.equal(a, b), i
     for i, (a, b) in enumerate(zip(out["0"], out["1"])):
         if i < 3:                                   # forward: always bitwise
             dd = (a.float() - b.float()).abs()
