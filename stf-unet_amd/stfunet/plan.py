@@ -103,6 +103,7 @@ class StepRuntime:
     def __init__(self, prog):
         self.prog = prog
         self.warm = int(os.environ.get("STF_PLAN_WARM", "1"))
+        self._bufs = None
         self._reset()
 
     def _reset(self):
@@ -121,9 +122,14 @@ class StepRuntime:
     # ------------------------------------------------------------------ signatures
     def _signature(self, x, training):
         p = self.prog
-        m = p.m
+        if self._bufs is None:
+            # (module, name) of every buffer, walked once: checking the slots per step costs
+            # ~20 us instead of ~0.5 ms for module.buffers() over the STF module tree
+            self._bufs = [(mod, n) for mod in p.m.modules() for n in mod._buffers
+                          if mod._buffers[n] is not None]
+        bufs = tuple(mod._buffers[n].data_ptr() for mod, n in self._bufs)
         return (tuple(x.shape), x.dtype, x.device, training, _lib.storage_dtype(), _lib.stream(),
-                p.flat.data.data_ptr(), tuple(b.data_ptr() for b in m.buffers()))
+                p.flat.data.data_ptr(), bufs)
 
     # ------------------------------------------------------------------ forward
     def busy(self):
