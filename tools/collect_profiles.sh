@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round profile collection (GPU box, repo root), all on ONE box so the numbers agree:
 #   1. the bench lines (python bench.py [--model stf], default steps)
-#   2. rocprofv3 --kernel-trace --stats of the SAME commands (per-kernel averages that
-#      the bench line's roofline avg_launch_us is checked against)
+#   2. rocprofv3 --kernel-trace --stats of the same workloads (per-kernel averages that
+#      the bench line's roofline avg_launch_us is checked against; without the dice / CPU
+#      legs, whose training steps would mix other shapes into the statistics)
 #   3. the two PMC passes (HBM traffic, tools/pmc_passes.sh) per model -> pmc_traffic_*.json
 #   4. the PK-map fit bench (tools/bench_pk.py) under rocprofv3, the eval-metric micro-bench
 # Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
@@ -18,11 +19,11 @@ timeout -k 10 600 python3 bench.py --config 5 --steps 10 --warmup 3 > $out/bench
 timeout -k 10 600 python3 bench.py --dtype fp16 --no-cpu-baseline > $out/bench_unet256_b64_fp16.json 2> $out/bench_unet16.err
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/unet -o run -- \
-  python3 $root/bench.py > $out/unet_rocprof_bench.json 2> $out/unet.log
+  python3 $root/bench.py --no-dice --no-cpu-baseline > $out/unet_rocprof_bench.json 2> $out/unet.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stf -o run -- \
-  python3 $root/bench.py --model stf > $out/stf_rocprof_bench.json 2> $out/stf.log
+  python3 $root/bench.py --model stf --no-dice --no-cpu-baseline > $out/stf_rocprof_bench.json 2> $out/stf.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/cfg5 -o run -- \
-  python3 $root/bench.py --config 5 --steps 10 --warmup 3 --no-cpu-baseline > $out/cfg5_rocprof_bench.json 2> $out/cfg5.log
+  python3 $root/bench.py --config 5 --steps 10 --warmup 3 --no-dice --no-cpu-baseline > $out/cfg5_rocprof_bench.json 2> $out/cfg5.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pk -o run -- \
   python3 $root/tools/bench_pk.py > $out/bench_pk.json 2> $out/pk.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/aug -o run -- \
