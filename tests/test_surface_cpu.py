@@ -245,3 +245,30 @@ def test_epoch_results_file_and_checkpoint_dict(tmp_path):
     assert all(torch.equal(a, b) for a, b in zip(m.state_dict().values(), m2.state_dict().values()))
     es = engine.EarlyStopping(patience=2)
     assert [es.step(v) for v in (0.5, 0.6, 0.6, 0.55)] == [False, False, False, True] and es.early_stop
+
+
+def test_plan_bookkeeping_on_host():
+    """The launch-plan entry points' host-side state machine (no launches: CPU-only):
+    one recording per thread, stop without record refused, empty ranges replay, out-of-range
+    replays refused, timing of an untimed plan is empty."""
+    import ctypes
+    from stfunet import _lib
+    lib = _lib.load()
+    einval = 100001
+    h = lib.stf_plan_create()
+    assert h and lib.stf_plan_size(h) == 0
+    assert lib.stf_plan_stop() == einval
+    assert lib.stf_plan_record(h) == 0
+    assert lib.stf_plan_record(h) == einval                # one recording per thread
+    assert lib.stf_plan_tag(b"igemm", 1.0) == 0 and lib.stf_plan_tag_end() == 0
+    assert lib.stf_plan_replay(h, 0, 0, None) == einval    # not while it records
+    assert lib.stf_plan_stop() == 0
+    assert lib.stf_plan_size(h) == 0
+    assert lib.stf_plan_replay(h, 0, 0, None) == 0
+    assert lib.stf_plan_replay(h, 0, 1, None) == einval
+    assert lib.stf_plan_replay(h, 1, 0, None) == einval
+    n, ms, fl = ctypes.c_int(-1), ctypes.c_double(-1), ctypes.c_double(-1)
+    assert lib.stf_plan_timing(h, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(fl)) == 0
+    assert (n.value, ms.value, fl.value) == (0, 0.0, 0.0)
+    assert lib.stf_plan_tag(b"outside", 1.0) == 0           # a tag outside a recording is ignored
+    lib.stf_plan_destroy(h)
