@@ -31,6 +31,7 @@ number of eager steps before recording (default 1).
 import ctypes
 import os
 import weakref
+from collections import OrderedDict
 
 import torch
 
@@ -96,18 +97,10 @@ def _pool_ctx():
     return pool, torch.cuda.use_mem_pool(pool)
 
 
-class StepRuntime:
-    """Plan cache of one program (UNetProgram / STFProgram): the training step's forward
-    and backward, recorded at the ``warm``-th step of a signature and replayed after."""
+class _Entry:
+    """One signature's recorded step: its plans, static buffers and private pool."""
 
-    def __init__(self, prog):
-        self.prog = prog
-        self.warm = int(os.environ.get("STF_PLAN_WARM", "1"))
-        self._bufs = None
-        self._reset()
-
-    def _reset(self):
-        self.sig = None
+    def __init__(self):
         self.seen = 0
         self.fwd = self.bwd = None
         self.x = self.logits = self.S = None
@@ -118,6 +111,36 @@ class StepRuntime:
         self.bkeep = []
         self.pool = None
         self.owner = None      # weakref to the autograd ctx holding the static S until its backward
+
+    def busy(self):
+        """The static buffers still belong to an earlier forward whose backward has not run
+        (two forwards before their backwards): a new forward must not overwrite them."""
+        o = self.owner() if self.owner is not None else None
+        return o is not None and self.S is not None and getattr(o, "saved", None) is self.S
+
+
+class StepRuntime:
+    """Plan cache of one program (UNetProgram / STFProgram): per signature the training step's
+    forward and backward, recorded at the ``warm``-th step of that signature and replayed after.
+    Up to ``STF_PLAN_SLOTS`` (default 2) signatures stay recorded, least recently used evicted:
+    an epoch's smaller last batch gets its own plan instead of throwing away the full batch's."""
+
+    def __init__(self, prog):
+        self.prog = prog
+        self.warm = int(os.environ.get("STF_PLAN_WARM", "1"))
+        self.slots = max(1, int(os.environ.get("STF_PLAN_SLOTS", "2")))
+        self._bufs = None
+        self.entries = OrderedDict()
+        self.cur = None         # entry of the last planned forward
+
+    # the most recent entry's plans (bench.py / tests)
+    @property
+    def fwd(self):
+        return self.cur.fwd if self.cur is not None else None
+
+    @property
+    def bwd(self):
+        return self.cur.bwd if self.cur is not None else None
 
     # ------------------------------------------------------------------ signatures
     def _signature(self, x, training):
@@ -131,79 +154,85 @@ class StepRuntime:
         return (tuple(x.shape), x.dtype, x.device, training, _lib.storage_dtype(), _lib.stream(),
                 p.flat.data.data_ptr(), bufs)
 
-    # ------------------------------------------------------------------ forward
-    def busy(self):
-        """The static buffers still belong to an earlier forward whose backward has not run
-        (two forwards before their backwards): a new forward must not overwrite them."""
-        o = self.owner() if self.owner is not None else None
-        return o is not None and self.S is not None and getattr(o, "saved", None) is self.S
+    def _entry(self, sig):
+        e = self.entries.get(sig)
+        if e is None:
+            while len(self.entries) >= self.slots:
+                _, old = self.entries.popitem(last=False)
+                if old is self.cur:
+                    self.cur = None
+            e = self.entries[sig] = _Entry()
+        else:
+            self.entries.move_to_end(sig)
+        return e
 
+    # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd, ctx=None):
         """The program's forward(x, training, need_bwd) through the plan cache; only the
         training step (training and need_bwd) is planned, everything else runs eagerly.
         ``ctx``: the autograd ctx that will hold the returned state until its backward."""
         p = self.prog
-        if not (enabled() and training and need_bwd and nhwc.TIMER is None) or self.busy():
+        if not (enabled() and training and need_bwd and nhwc.TIMER is None):
             return p.forward(x, training, need_bwd)
-        if ctx is not None:
-            self.owner = weakref.ref(ctx)
-        sig = self._signature(x, training)
-        if sig != self.sig:
-            self._reset()
-            self.sig = sig
-        if self.fwd is None:
-            self.seen += 1
-            if self.seen <= self.warm:
+        e = self._entry(self._signature(x, training))
+        if e.busy():
+            return p.forward(x, training, need_bwd)
+        if e.fwd is None:
+            e.seen += 1
+            if e.seen <= self.warm:
                 return p.forward(x, training, need_bwd)
-            return self._record_forward(x, training)
-        self.x.copy_(x)
-        self.fwd.replay()
-        return self.logits, self.S
+            self._record_forward(e, x, training)
+        else:
+            e.x.copy_(x)
+            e.fwd.replay()
+        if ctx is not None:
+            e.owner = weakref.ref(ctx)
+        self.cur = e
+        return e.logits, e.S
 
-    def _record_forward(self, x, training):
+    def _record_forward(self, e, x, training):
         pool, ctx = _pool_ctx()
-        self.pool = pool
-        keep = self.keep = []
-        nhwc.KEEP = keep
+        e.pool = pool
+        nhwc.KEEP = e.keep
         try:
             if ctx is not None:
                 ctx.__enter__()
             try:
-                self.x = nhwc.empty(tuple(x.shape), x.dtype, x.device)
-                self.x.copy_(x)
+                e.x = nhwc.empty(tuple(x.shape), x.dtype, x.device)
+                e.x.copy_(x)
                 plan = Plan()
-                logits, S = plan.record(lambda: self.prog.forward(self.x, training, True))
+                e.logits, e.S = plan.record(lambda: self.prog.forward(e.x, training, True))
             finally:
                 if ctx is not None:
                     ctx.__exit__(None, None, None)
         finally:
             nhwc.KEEP = None
-        self.fwd, self.logits, self.S = plan, logits, S
-        return logits, S
+        e.fwd = plan
 
     # ------------------------------------------------------------------ backward
     def backward(self, S, dlogits):
         p = self.prog
-        if self.fwd is None or S is not self.S or not enabled() or nhwc.TIMER is not None:
+        e = next((v for v in self.entries.values() if v.fwd is not None and v.S is S), None)
+        if e is None or not enabled() or nhwc.TIMER is not None:
             return p.backward(S, dlogits)
         bsig = (tuple(dlogits.shape), p.flat.grad.data_ptr(), p.grad_ready_hook is not None, _lib.stream())
-        if self.bwd is None or bsig != self.bsig:
-            return self._record_backward(S, dlogits, bsig)
-        self.dl.copy_(dlogits)
+        if e.bwd is None or bsig != e.bsig:
+            return self._record_backward(e, S, dlogits, bsig)
+        e.dl.copy_(dlogits)
         pos = 0
         hook = p.grad_ready_hook
-        for idx, off in self.marks:
-            self.bwd.replay(pos, idx)
+        for idx, off in e.marks:
+            e.bwd.replay(pos, idx)
             hook(off)
             pos = idx
-        self.bwd.replay(pos)
+        e.bwd.replay(pos)
 
-    def _record_backward(self, S, dlogits, bsig):
+    def _record_backward(self, e, S, dlogits, bsig):
         p = self.prog
-        self.bwd = None
-        self.bkeep = []
-        nhwc.KEEP = self.bkeep
-        ctx = torch.cuda.use_mem_pool(self.pool) if self.pool is not None else None
+        e.bwd = None
+        e.bkeep = []
+        nhwc.KEEP = e.bkeep
+        ctx = torch.cuda.use_mem_pool(e.pool) if e.pool is not None else None
         plan = Plan()
         marks = []
         real_hook = p.grad_ready_hook
@@ -216,24 +245,25 @@ class StepRuntime:
             if ctx is not None:
                 ctx.__enter__()
             try:
-                self.dl = nhwc.empty(tuple(dlogits.shape), dlogits.dtype, dlogits.device)
-                self.dl.copy_(dlogits)
-                plan.record(lambda: p.backward(S, self.dl))
+                e.dl = nhwc.empty(tuple(dlogits.shape), dlogits.dtype, dlogits.device)
+                e.dl.copy_(dlogits)
+                plan.record(lambda: p.backward(S, e.dl))
             finally:
                 if ctx is not None:
                     ctx.__exit__(None, None, None)
         finally:
             nhwc.KEEP = None
             p.grad_ready_hook = real_hook
-        self.bwd, self.bsig, self.marks = plan, bsig, marks
+        e.bwd, e.bsig, e.marks = plan, bsig, marks
 
     def timing(self):
         """Summed (launches, ms, flops) of the TIMED kernel in this runtime's replays."""
         tot = [0, 0.0, 0.0]
-        for pl in (self.fwd, self.bwd):
-            if pl is not None:
-                n, ms, fl = pl.timing()
-                tot[0] += n
-                tot[1] += ms
-                tot[2] += fl
+        for e in self.entries.values():
+            for pl in (e.fwd, e.bwd):
+                if pl is not None:
+                    n, ms, fl = pl.timing()
+                    tot[0] += n
+                    tot[1] += ms
+                    tot[2] += fl
         return tuple(tot)

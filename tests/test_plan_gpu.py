@@ -114,7 +114,9 @@ def test_plan_hook_segments(which):
 
 
 def test_plan_rerecords_on_shape_change():
-    """A new batch shape is a new signature: eager warm-up, a new recording, then replays."""
+    """A new batch shape is a new signature: eager warm-up, its own recording, then replays; the
+    previous shape's plan stays cached (an epoch's smaller last batch must not cost the full batch
+    its plan), and a replayed step's gradient equals an eager one."""
     from stfunet import engine
     os.environ["STF_PLAN"] = "1"
     try:
@@ -123,18 +125,22 @@ def test_plan_rerecords_on_shape_change():
         big = _batches("unet", 2, b=3, hw=64)
         rt = model.program.runtime
         plans = []
-        for i, (x, t) in enumerate(small * 2 + big * 2):
+        for x, t in small * 2 + big * 2 + small * 2:
             for p in model.parameters():
                 p.grad = None
             loss = engine.criterion(model(x), t)
             loss.backward()
             plans.append(rt.fwd)
-        assert plans[0] is None and plans[1] is not None and plans[2] is plans[1] and plans[3] is plans[1]
-        assert plans[4] is None and plans[5] is not None and plans[5] is not plans[1]
-        # the replayed big-batch gradient equals an eager one from the same weights
+        p_small, p_big = plans[1], plans[5]
+        assert plans[0] is None and p_small is not None and plans[2] is p_small and plans[3] is p_small
+        assert plans[4] is p_small                     # the big shape's eager warm-up step
+        assert p_big is not None and p_big is not p_small and plans[6] is p_big and plans[7] is p_big
+        assert plans[8] is p_small and plans[9] is p_small        # back to small: no re-recording
+        assert len(rt.entries) == 2
+        # the replayed small-batch gradient equals an eager one from the same weights
         g_plan = model.program.flat.grad.clone()
         os.environ["STF_PLAN"] = "0"
-        x, t = big[1]
+        x, t = small[1]
         model.program.flat.grad.zero_()
         for p in model.parameters():
             p.grad = None
