@@ -348,6 +348,23 @@ int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, void* out, voi
                        stf_stream_t stream);
 int stf_maxpool3s2_bwd(const void* argmax, const void* dout, int N, int H, int W, int C, void* dx,
                        stf_stream_t stream);
+/* The stem's BatchNorm + ReLU and that max pool in one pass (src/stf_lstm_unet.py:178-180):
+ * pooled out and argmax exactly as stf_bn_act (scale / shift of group n / (N / groups), ReLU,
+ * 16-bit rounding) followed by stf_maxpool3s2_fwd, without writing the activation.  ABI v11. */
+int stf_bn_act_maxpool3s2(const void* y, int N, int H, int W, int C, int groups, const float* scale,
+                          const float* shift, void* out, void* argmax, stf_stream_t stream);
+/* The stem BatchNorm's backward through that max pool: the gradient of each pixel is gathered
+ * from the pooled gradient dout [N][Ho][Wo][C] over the <= 4 windows whose recorded argmax it
+ * is (rounded to 16 bits, as stf_maxpool3s2_bwd stores it), masked by the ReLU recomputed from
+ * y; reduce -> partials as stf_bn_bwd_reduce (then stf_bn_bwd_finalize), apply -> dy, without
+ * the full-size d(activation) tensor.  Same values as stf_maxpool3s2_bwd + stf_bn_bwd_reduce
+ * (mask_mode 1) + stf_bn_bwd_apply.  ABI v11. */
+int stf_bn_bwd_reduce_pool3(const void* argmax, const void* dout, const void* y, int N, int H, int W, int C,
+                            int groups, const float* scale, const float* shift, const float* mean,
+                            const float* invstd, float* partial, stf_stream_t stream);
+int stf_bn_bwd_apply_pool3(const void* argmax, const void* dout, const void* y, int N, int H, int W, int C,
+                           int groups, const float* scale, const float* shift, const float* coef, void* dy,
+                           stf_stream_t stream);
 /* nn.LSTM(C, C) weights -> gate-interleaved GEMM operands: wcat [4C][2C] (row
  * 4c+q = torch row q*C+c of [W_ih | W_hh]), wcat_t [2C][4C], bias = b_ih + b_hh
  * interleaved (src/stf_lstm_unet.py:124-127).  C in {16, 32, ..., 512} (STF_EINVAL otherwise). */

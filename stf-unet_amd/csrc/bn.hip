@@ -714,6 +714,141 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in
   }
 }
 
+// ------------------------------------------------------------------ stem: BN backward through MaxPool(3,2,1)
+// g of the stem's BatchNorm backward gathered straight from its max pool's backward: the sum of
+// dout over the <= 4 windows whose recorded first maximum (argmax, index dy*3+dx) is this pixel,
+// in the order stf_maxpool3s2_bwd adds them, rounded to the 16-bit storage -- so the values equal
+// maxpool3s2_bwd + the mask-recomputing reduce / apply without writing or reading d a0.  A unit is
+// a 2x2 block of input pixels (2by + a, 2bx + b): the windows (by + {0,1}, bx + {0,1}) cover all
+// four, so each window's argmax and dout are loaded once per block (9 window reads for the four
+// pixels in the per-pixel gather).
+// APPLY = false: the (sum g, sum g*xhat) partials of bn_bwd_reduce_g_kernel<1>;
+// APPLY = true: dy = A*g' + B*y + C with the ReLU mask recomputed (bn_bwd_apply_g_kernel<true>)
+template <bool APPLY>
+__global__ __launch_bounds__(NT) void bn_bwd_pool3_kernel(const uint8_t* __restrict__ argmax,
+                                                          const uint16_t* __restrict__ dout,
+                                                          const uint16_t* __restrict__ y, int H, int W, int Ho,
+                                                          int Wo, int ipg, int cgs, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ coef, uint16_t* __restrict__ dy,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[APPLY ? 1 : NT][17];
+  const int g = blockIdx.y, CG = 1 << cgs, C = 8 << cgs;
+  const int H2 = (H + 1) >> 1, W2 = (W + 1) >> 1;
+  const int bpi = H2 * W2;                               // 2x2 blocks per image
+  const int upg = (ipg * bpi) << cgs, S = gridDim.x * NT;
+  const int u0 = blockIdx.x * NT + threadIdx.x;
+  const int cg = threadIdx.x & (CG - 1);
+  float sc[8], sh[8], mu[8], is[8], A[8], B[8], Cc[8];
+  load_affine(scale + (size_t)g * C, cg * 8, sc);
+  load_affine(shift + (size_t)g * C, cg * 8, sh);
+  if (APPLY) {
+    load_affine(coef + (size_t)g * 3 * C, cg * 8, A);
+    load_affine(coef + (size_t)g * 3 * C + C, cg * 8, B);
+    load_affine(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
+  } else {
+    load_affine(mean + (size_t)g * C, cg * 8, mu);
+    load_affine(invstd + (size_t)g * C, cg * 8, is);
+  }
+  float sg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // U units per iteration, all their loads issued before any use (the reduce runs <= 1024
+  // blocks -- the finalize's row budget -- so it needs the memory-level parallelism per thread)
+  constexpr int U = APPLY ? 1 : 2;
+  for (int u = u0; u < upg; u += S * U) {
+    uint2 am[U][2][2];
+    uint4 dr[U][2][2], yr[U][2][2];
+    int nn[U], bys[U], bxs[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int uk = u + k * S;
+      const int b = uk >> cgs;
+      const int n = g * ipg + b / bpi, rb = b - (b / bpi) * bpi;
+      const int by = rb / W2, bx = rb - by * W2;
+      nn[k] = uk < upg ? n : -1;
+      bys[k] = by;
+      bxs[k] = bx;
+      // the four windows (by + wy, bx + wx): argmax (8 channel bytes) and dout (8 channels),
+      // and the block's four pixels of y
+#pragma unroll
+      for (int wy = 0; wy < 2; ++wy)
+#pragma unroll
+        for (int wx = 0; wx < 2; ++wx) {
+          const int oy = by + wy, ox = bx + wx;
+          if (uk < upg && oy < Ho && ox < Wo) {
+            const long wo = (((long)n * Ho + oy) * Wo + ox) * C + cg * 8;
+            am[k][wy][wx] = *reinterpret_cast<const uint2*>(argmax + wo);
+            dr[k][wy][wx] = *reinterpret_cast<const uint4*>(dout + wo);
+          } else {
+            am[k][wy][wx] = make_uint2(0xffffffffu, 0xffffffffu);    // matches no pixel
+            dr[k][wy][wx] = make_uint4(0, 0, 0, 0);
+          }
+          const int iy = 2 * by + wy, ix = 2 * bx + wx;
+          if (uk < upg && iy < H && ix < W)
+            yr[k][wy][wx] = *reinterpret_cast<const uint4*>(y + (((size_t)n * H + iy) * W + ix) * C + cg * 8);
+          else
+            yr[k][wy][wx] = make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (nn[k] < 0) continue;
+      const int n = nn[k], by = bys[k], bx = bxs[k];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int iy = 2 * by + a, ix = 2 * bx + bb;
+          if (iy >= H || ix >= W) continue;
+          float v[8], gq[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          unpack8(yr[k][a][bb], v);
+          // windows of pixel row iy: oy = by (always) and by + 1 (odd iy); same for x; ascending
+#pragma unroll
+          for (int wy = 0; wy < 2; ++wy) {
+            if (wy > a) continue;
+#pragma unroll
+            for (int wx = 0; wx < 2; ++wx) {
+              if (wx > bb) continue;
+              const uint32_t me = (uint32_t)((iy - 2 * (by + wy) + 1) * 3 + (ix - 2 * (bx + wx) + 1));
+              float d[8];
+              unpack8(dr[k][wy][wx], d);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const uint32_t q = ((j < 4 ? am[k][wy][wx].x : am[k][wy][wx].y) >> (8 * (j & 3))) & 0xffu;
+                if (q == me) gq[j] += d[j];
+              }
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gr = round_e(gq[j]);
+            const float gj = (v[j] * sc[j] + sh[j] > 0.f) ? gr : 0.f;
+            if (APPLY) gq[j] = A[j] * gj + B[j] * v[j] + Cc[j];
+            else {
+              sg[j] += gj;
+              sgx[j] += gj * (v[j] - mu[j]) * is[j];
+            }
+          }
+          if (APPLY)
+            *reinterpret_cast<uint4*>(dy + (((size_t)n * H + iy) * W + ix) * C + cg * 8) = pack8(gq);
+        }
+    }
+  }
+  if (APPLY) return;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
+  __syncthreads();
+  const size_t row = (size_t)g * gridDim.x + blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int gg = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int t = gg; t < NT; t += CG) { a += red[t][j]; b += red[t][8 + j]; }
+    partial[row * 2 * C + c] = a;
+    partial[row * 2 * C + C + c] = b;
+  }
+}
+
 }  // namespace
 
 // the group-major kernels (STF_BN_G=0: the per-unit-division kernels, A/B); usable when C / 8 is
@@ -941,5 +1076,44 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
     hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+// BatchNorm backward of the STF stem through its MaxPool(3,2,1) (src/stf_lstm_unet.py:178-180):
+// the incoming gradient is the pooled output's (dout [N][Ho][Wo][C]) routed by the forward's
+// argmax (stf_bn_act_maxpool3s2 / stf_maxpool3s2_fwd), never materialized at full size.
+// Partials as stf_bn_bwd_reduce (rows per group = stf_bn_bwd_tiles(N, H, W, C, groups, 0)).
+extern "C" int stf_bn_bwd_reduce_pool3(const void* argmax, const void* dout, const void* y, int N, int H, int W,
+                                       int C, int groups, const float* scale, const float* shift,
+                                       const float* mean, const float* invstd, float* partial,
+                                       stf_stream_t stream) {
+  const long Mg = (long)N * H * W / (groups > 0 ? groups : 1);
+  if (!argmax || !dout || !y || !partial || groups < 1 || N % groups || !bn_g_ok(Mg, C) ||
+      (long)N * H * W >= (1L << 31))
+    return STF_EINVAL;
+  const int tpg = stf_bn_bwd_tiles(N, H, W, C, groups, 0);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipLaunchKernelGGL(bn_bwd_pool3_kernel<false>, dim3(tpg, groups), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint8_t*)argmax, (const uint16_t*)dout, (const uint16_t*)y, H, W, Ho, Wo, N / groups,
+                     log2i(C / 8), scale, shift, mean, invstd, (const float*)nullptr, (uint16_t*)nullptr, partial);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+// dy = A g' + B y + C (coef from stf_bn_bwd_finalize), g' = the routed gradient masked by the ReLU.
+extern "C" int stf_bn_bwd_apply_pool3(const void* argmax, const void* dout, const void* y, int N, int H, int W,
+                                      int C, int groups, const float* scale, const float* shift, const float* coef,
+                                      void* dy, stf_stream_t stream) {
+  const long Mg = (long)N * H * W / (groups > 0 ? groups : 1);
+  if (!argmax || !dout || !y || !coef || !dy || groups < 1 || N % groups || !bn_g_ok(Mg, C) ||
+      (long)N * H * W >= (1L << 31))
+    return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long units = (long)(N / groups) * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  const dim3 grid(g_tiles(units, groups, 8192) * UPT, groups);
+  hipLaunchKernelGGL(bn_bwd_pool3_kernel<true>, grid, dim3(NT), 0, (hipStream_t)stream, (const uint8_t*)argmax,
+                     (const uint16_t*)dout, (const uint16_t*)y, H, W, Ho, Wo, N / groups, log2i(C / 8), scale, shift,
+                     (const float*)nullptr, (const float*)nullptr, coef, (uint16_t*)dy, (float*)nullptr);
+  STF_CHECK_LAUNCH();
   return 0;
 }

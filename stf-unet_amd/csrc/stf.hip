@@ -128,6 +128,61 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
   }
 }
 
+// The stem's BatchNorm + ReLU fused into its max pool (src/stf_lstm_unet.py:178-180): each
+// window tap is relu(y*scale[g]+shift[g]) rounded to the 16-bit storage -- exactly the value
+// stf_bn_act would have stored in the activation a0 -- so the pooled output and the recorded
+// argmax equal bn_act followed by maxpool3_fwd bit for bit, and a0 (4x the pooled bytes) is never
+// written nor read back.  g = n / ipg (per-time-step statistics of the encoder).
+__global__ void bn_act_maxpool3_kernel(const uint16_t* __restrict__ y, int N, int H, int W, int C, int Ho, int Wo,
+                                       int ipg, const float* __restrict__ scale, const float* __restrict__ shift,
+                                       uint16_t* __restrict__ out, uint8_t* __restrict__ argmax) {
+  const int CG = C / 8;
+  const long units = (long)N * Ho * Wo * CG;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long p = u / CG;
+    const int n = (int)(p / ((long)Ho * Wo));
+    const int rem = (int)(p - (long)n * Ho * Wo);
+    const int oy = rem / Wo, ox = rem - oy * Wo;
+    const int g = n / ipg;
+    float sc[8], sh[8];
+    {
+      const float4 a = *reinterpret_cast<const float4*>(scale + (size_t)g * C + cg * 8);
+      const float4 b = *reinterpret_cast<const float4*>(scale + (size_t)g * C + cg * 8 + 4);
+      const float4 c = *reinterpret_cast<const float4*>(shift + (size_t)g * C + cg * 8);
+      const float4 d = *reinterpret_cast<const float4*>(shift + (size_t)g * C + cg * 8 + 4);
+      sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+      sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+    }
+    float mx[8];
+    int am[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = -1; }
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = 2 * oy - 1 + dy;
+      if (iy < 0 || iy >= H) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ix = 2 * ox - 1 + dx;
+        if (ix < 0 || ix >= W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + (((long)n * H + iy) * W + ix) * C + cg * 8), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = round_e(fmaxf(v[j] * sc[j] + sh[j], 0.f));     // bn_act's stored value
+          if (a > mx[j] || am[j] < 0) { mx[j] = a; am[j] = dy * 3 + dx; }
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(out + p * C + cg * 8) = pack8(mx);
+    if (argmax) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[4 + j] << (8 * j); }
+      *reinterpret_cast<uint2*>(argmax + p * C + cg * 8) = make_uint2(lo, hi);
+    }
+  }
+}
+
 // gather form of the backward: every input pixel sums dout over the (<= 4)
 // windows whose recorded first maximum is this pixel -- no atomics, fixed order
 __global__ void maxpool3_bwd_kernel(const uint8_t* __restrict__ argmax, const uint16_t* __restrict__ dout, int N,
@@ -274,6 +329,18 @@ extern "C" int stf_maxpool3s2_fwd(const void* x, int N, int H, int W, int C, voi
   const long units = (long)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(maxpool3_fwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
                      (const uint16_t*)x, N, H, W, C, Ho, Wo, (uint16_t*)out, (uint8_t*)argmax);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_bn_act_maxpool3s2(const void* y, int N, int H, int W, int C, int groups, const float* scale,
+                                     const float* shift, void* out, void* argmax, stf_stream_t stream) {
+  if (C % 8 || groups < 1 || N % groups || !y || !scale || !shift || !out) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long units = (long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(bn_act_maxpool3_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)y, N, H, W, C, Ho, Wo, N / groups, scale, shift, (uint16_t*)out,
+                     (uint8_t*)argmax);
   STF_CHECK_LAUNCH();
   return 0;
 }

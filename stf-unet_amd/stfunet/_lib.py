@@ -113,6 +113,9 @@ _SIGS = {
                                 P]),
     "stf_maxpool3s2_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
+    "stf_bn_act_maxpool3s2": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
+    "stf_bn_bwd_reduce_pool3": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P, P]),
+    "stf_bn_bwd_apply_pool3": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "stf_lstm_pack": (c_int, [P, P, P, P, c_int, P, P, P, P]),
     "stf_lstm_unpack_grad": (c_int, [P, P, c_int, P, P, P, P, P]),
     "stf_lstm_seq_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P]),

@@ -696,6 +696,44 @@ def bn_backward_fused(dz: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, d
                                     mask_relu=relu)
 
 
+def bn_backward_maxpool3(y: Feat, st: BNState, bn, dgamma, dbeta, argmax, dpool: Feat):
+    """Backward of maxpool3s2(relu(BN(y))) w.r.t. y (the STF stem): the pooled gradient is
+    routed by the forward's argmax inside the reduce and apply passes (stf_bn_bwd_*_pool3),
+    never materialized at full size.  Returns dy."""
+    y.check()
+    dpool.check()
+    C, dev, G = y.C, y.buf.device, st.groups
+    assert y.cs == C and y.off == 0 and dpool.cs == C and dpool.off == 0
+    assert (dpool.N, dpool.H, dpool.W) == (y.N, (y.H - 1) // 2 + 1, (y.W - 1) // 2 + 1)
+    tiles = _lib.load().stf_bn_bwd_tiles(y.N, y.H, y.W, C, G, 0)
+    part = empty(G * tiles * 2 * C, torch.float32, dev)
+    call("stf_bn_bwd_reduce_pool3", _p(argmax), dpool.ptr(), y.ptr(), y.N, y.H, y.W, C, G, _p(st.scale),
+         _p(st.shift), _p(st.mean), _p(st.invstd), _p(part), stream())
+    coef = _bn_bwd_coef(y, st, bn, part, tiles, dgamma, dbeta)
+    dy = new_feat(y.N, y.H, y.W, C, dev)
+    call("stf_bn_bwd_apply_pool3", _p(argmax), dpool.ptr(), y.ptr(), y.N, y.H, y.W, C, G, _p(st.scale),
+         _p(st.shift), _p(coef), dy.ptr(), stream())
+    return dy
+
+
+def _bn_bwd_coef(y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta):
+    """stf_bn_bwd_finalize: dy = A g + B y + C coefficients [G][3][C] from the partial sums
+    (dgamma / dbeta written, or parked for flush_bn_grads when grouped; eval mode: A only)."""
+    C, dev, G = y.C, y.buf.device, st.groups
+    coef = empty(G * 3 * C, torch.float32, dev)
+    if G > 1 and (dgamma is not None or dbeta is not None):
+        _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
+                                        dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
+        dgamma = dbeta = None
+    call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean),
+         _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
+    if not st.training:
+        cv = coef.view(G, 3, C)
+        cv[:, 0].copy_(bn.weight.detach() * st.invstd)
+        cv[:, 1:].zero_()
+    return coef
+
+
 def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dgamma, dbeta, dbias=None,
                              out: Feat = None, mask_relu=False):
     """Finalize + apply.  ``mask_relu``: g is the raw incoming gradient and the

@@ -426,14 +426,16 @@ class STFProgram:
             stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, kpad), 64, y0, 1, 1,
                                       1, 0, want_stats=training, groups=T)
         S.bn0 = nhwc.bn_finalize(stats, tiles, m.bn1, y0.M, training, T)
-        a0 = new_feat(N, h2, w2, 64, dev)
-        nhwc.bn_act(y0, S.bn0, a0)
         h4, w4 = (h2 - 1) // 2 + 1, (w2 - 1) // 2 + 1
         p0 = new_feat(N, h4, w4, 64, dev)
         # the window argmax the backward routes through (eval-mode backward needs it too)
         S.pool_arg = nhwc.empty(N * h4 * w4 * 64, torch.uint8, dev) if need_bwd else None
-        call("stf_maxpool3s2_fwd", a0.ptr(), N, h2, w2, 64, p0.ptr(), _p(S.pool_arg), stream())
-        S.xin, S.y0, S.a0, S.p0 = xin, y0, a0, p0
+        # bn1 + relu + maxpool in one pass: the activation relu(bn1(y0)) is never stored (the
+        # backward needs only y0 and the argmax)
+        y0.check()
+        call("stf_bn_act_maxpool3s2", y0.ptr(), N, h2, w2, 64, T, _p(S.bn0.scale), _p(S.bn0.shift), p0.ptr(),
+             _p(S.pool_arg), stream())
+        S.xin, S.y0, S.p0 = xin, y0, p0
         # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat);
         # lstm li (li < 3) starts on its side stream as soon as layer li is done
         S.enc, S.lbuf, S.pkbuf = [], [], []
@@ -602,9 +604,9 @@ class STFProgram:
                     dout = bp.backward(s, gv, dout=dout)
             self._done(getattr(m, f"layer{li + 1}"))
         # stem: maxpool(3,2,1) <- relu(bn1(conv1 x))
-        da0 = new_feat(S.a0.N, S.a0.H, S.a0.W, 64, dev)
-        call("stf_maxpool3s2_bwd", _p(S.pool_arg), dout.ptr(), S.a0.N, S.a0.H, S.a0.W, 64, da0.ptr(), stream())
-        dy0 = nhwc.bn_backward(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), dz=da0)
+        # the pooled gradient routed by the argmax inside the BN backward's passes (no full-size
+        # d relu(bn1(y0)) tensor)
+        dy0 = nhwc.bn_backward_maxpool3(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), S.pool_arg, dout)
         w1 = m.conv1.weight
         kreal = w1[0].numel()
         if S.stem_gather:                      # 8-channel packed input, 7x7/s2 gather

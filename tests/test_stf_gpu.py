@@ -505,3 +505,70 @@ def test_stf_input_gradient_rejected():
     x = torch.randn(1, 2, 1, 64, 64, device=DEV, requires_grad=True)
     with pytest.raises(NotImplementedError):
         m(x)
+
+
+def test_stem_bn_act_maxpool_fused_equals_two_passes():
+    """stf_bn_act_maxpool3s2 (the stem's BN + ReLU inside its MaxPool(3,2,1)) gives the pooled
+    output and the window argmax of stf_bn_act followed by stf_maxpool3s2_fwd bit for bit
+    (odd sizes: partial windows at the border; 3 statistics groups; ties from the ReLU zeros)."""
+    from stfunet import nhwc
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import BNState, _p
+    N, H, W, C, G = 6, 21, 18, 64, 3
+    y = nhwc.new_feat(N, H, W, C, DEV)
+    y.buf.normal_()
+    st = BNState(C, DEV, N * H * W, G)
+    st.scale.uniform_(0.5, 1.5)
+    st.shift.uniform_(-0.5, 0.5)
+    a = nhwc.new_feat(N, H, W, C, DEV)
+    nhwc.bn_act(y, st, a)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    p_ref = torch.empty(N * Ho * Wo * C, dtype=torch.bfloat16, device=DEV)
+    arg_ref = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=DEV)
+    call("stf_maxpool3s2_fwd", a.ptr(), N, H, W, C, _p(p_ref), _p(arg_ref), stream())
+    p = torch.empty_like(p_ref)
+    arg = torch.empty_like(arg_ref)
+    call("stf_bn_act_maxpool3s2", y.ptr(), N, H, W, C, G, _p(st.scale), _p(st.shift), _p(p), _p(arg), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(p.view(torch.int16), p_ref.view(torch.int16))
+    assert torch.equal(arg, arg_ref)
+
+
+def test_stem_bn_backward_through_maxpool():
+    """nhwc.bn_backward_maxpool3 (the pooled gradient routed by the argmax inside the BN
+    backward's reduce and apply: stf_bn_bwd_*_pool3) against stf_maxpool3s2_bwd + the
+    mask-recomputing nhwc.bn_backward it replaces: dy within bf16 rounding (the partial sums
+    are added in another order), dgamma / dbeta within 1e-4 relative."""
+    from stfunet import nhwc
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import BNState, _p
+    N, H, W, C, G = 8, 34, 29, 64, 4
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = nhwc.new_feat(N, H, W, C, DEV)
+    y.buf.normal_()
+    st = BNState(C, DEV, N * H * W, G)
+    st.scale.uniform_(0.5, 1.5)
+    st.shift.uniform_(-0.5, 0.5)
+    st.mean.normal_(0, 0.1)
+    st.invstd.uniform_(0.8, 1.2)
+    p0 = nhwc.new_feat(N, Ho, Wo, C, DEV)
+    arg = torch.empty(N * Ho * Wo * C, dtype=torch.uint8, device=DEV)
+    call("stf_bn_act_maxpool3s2", y.ptr(), N, H, W, C, G, _p(st.scale), _p(st.shift), p0.ptr(), _p(arg), stream())
+    dpool = nhwc.new_feat(N, Ho, Wo, C, DEV)
+    dpool.buf.normal_()
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    res = {}
+    for mode in ("old", "new"):
+        dg = torch.zeros(C, device=DEV)
+        db = torch.zeros(C, device=DEV)
+        if mode == "old":
+            da = nhwc.new_feat(N, H, W, C, DEV)
+            call("stf_maxpool3s2_bwd", _p(arg), dpool.ptr(), N, H, W, C, da.ptr(), stream())
+            dy = nhwc.bn_backward(y, st, bn, dg, db, dz=da)
+        else:
+            dy = nhwc.bn_backward_maxpool3(y, st, bn, dg, db, arg, dpool)
+        nhwc.flush_bn_grads()
+        res[mode] = (dy.dense(), dg.clone(), db.clone())
+    torch.cuda.synchronize()
+    assert rel(res["new"][0], res["old"][0]) < 5e-3
+    assert rel(res["new"][1], res["old"][1]) < 1e-4 and rel(res["new"][2], res["old"][2]) < 1e-4
