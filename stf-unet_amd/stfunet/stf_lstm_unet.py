@@ -353,9 +353,24 @@ class STFProgram:
         of each other: lstm k forward runs beside the deeper encoder layers and lstm k
         backward beside the remaining decoder backward, which leave most CUs idle at
         1/16 and 1/32 resolution (lstm4 stays on the main stream: the decoder and the
-        encoder backward need it first).  3 side streams + main = GPU_MAX_HW_QUEUES."""
+        encoder backward need it first).
+
+        ``STF_SIDE_STREAMS`` maps lstm 1-3 to streams, one character each: a digit names a
+        private stream, ``w`` the weight-gradient side stream (``nhwc.wgrad_side_stream``)."""
         if self._side is None or self._side[0].device != dev:
-            self._side = [torch.cuda.Stream(device=dev) for _ in range(3)]
+            spec = os.environ.get("STF_SIDE_STREAMS", "00w")
+            if len(spec) != 3 or any(c not in "012w" for c in spec):
+                raise ValueError(f"STF_SIDE_STREAMS={spec!r}: three of 0 1 2 w")
+            own, ws = {}, nhwc.wgrad_side_stream(dev)
+            side = []
+            for c in spec:
+                if c == "w" and ws is not None:
+                    side.append(ws)
+                else:
+                    if c not in own:
+                        own[c] = torch.cuda.Stream(device=dev)
+                    side.append(own[c])
+            self._side = side
         return self._side
 
     def _done(self, module):
