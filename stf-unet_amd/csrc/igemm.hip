@@ -903,6 +903,18 @@ __global__ __launch_bounds__(NT) void splitk_reduce_kernel(Geo a, int tpg) {
 // any tap shift (checked exhaustively over columns, shifts and row residues).
 STF_DEV int swzh(int key, int kc) { return kc ^ ((key >> 1) & 2); }
 
+// output row (pixel index of the destination) of tile pixel p, or -1 outside the image
+template <int PH, int PW, int IX>
+STF_DEV int halo_pixel(int p, int img, int ty, int tx, int Hd, int Wd) {
+  int y = ty * PH + p / PW, x = tx * PW + p % PW;
+  if constexpr (IX > 1) {
+    const int b = (p % PW) / (PW / IX);
+    x = p % PW - b * (PW / IX);
+    img += b;
+  }
+  return (y < Hd && x < Wd) ? (img * Hd + y) * Wd + x : -1;
+}
+
 // NW waves x 64 pixels = PH x PW tile; STAGES = 2: one 8-wave workgroup per CU
 // with a 2-stage ring; STAGES = 1: two 4-wave workgroups per CU, single stage
 // each, so one workgroup's DMA wait and epilogue overlap the other's MFMAs.
@@ -910,11 +922,17 @@ STF_DEV int swzh(int key, int kc) { return kc ^ ((key >> 1) & 2); }
 // row j*16 + fk*4 + r <- channel (j>>1)*32 + fk*8 + (j&1)*4 + r, so a lane's
 // accumulators of fragments (0,1) and (2,3) are 8 consecutive channels each and
 // the epilogue stores 16-B chunks straight from registers (no LDS staging).
-template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT = 0, bool BNR = false>
-__global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes,
-                                                                                    int TY, int TX, int per, int rem) {
+//
+// IX > 1 (multi-image tiles, conv3x3_halo2_kernel): the PH x PW tile is IX whole images of
+// PH x (PW / IX) side by side (STF layer3: two 16 x 16 images in one 16 x 32 tile), so a
+// small image fills the wide tile instead of half a 16 x 16 one: twice the pixels per stage
+// for the same weight rows.  Neighbouring images share one zero column in the halo (image
+// b's column x sits at halo column b * (IW + 1) + 1 + x), PW + IX + 1 columns in all.
+template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT, bool BNR, int IX>
+__device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int TX, int per, int rem) {
   constexpr int NTH = 64 * NW, BN = 64, RPI = 16;       // 64-B rows: 16 per 1-KiB DMA instruction
-  constexpr int HW = PW + 2, HR = (PH + 2) * HW;        // halo rows
+  constexpr int IW = PW / IX;                           // image width in a multi-image tile
+  constexpr int HW = PW + IX + 1, HR = (PH + 2) * HW;   // halo rows
   constexpr int HI = (HR + RPI * NW - 1) / (RPI * NW);  // halo DMA instructions per wave
   constexpr int WI = (9 * BN + RPI * NW - 1) / (RPI * NW);
   constexpr int HROWS = HI * RPI * NW, WROWS = WI * RPI * NW;
@@ -937,7 +955,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar DMA addressing
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
   const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
-  const int ntiles = a.N * tpi;                         // items: channel slice major, pixel tile minor
+  const int ntiles = (a.N / IX) * tpi;                  // items: channel slice major, pixel tile minor
   const int ipg = a.Mg / (a.Hd * a.Wd);                 // images per statistics group
   const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
   const int it0 = blockIdx.x * per + min((int)blockIdx.x, rem);
@@ -961,7 +979,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
   int wkey0 = -1, wkey1 = -1;
   auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1, bool wload) {
     const int nt = item / ntiles, tile = item - nt * ntiles;
-    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
     char* st = smem + buf * STAGE;
 #pragma unroll
@@ -969,10 +987,15 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       if (i < k0 || i >= k1) continue;
       const int hr = (wave * HI + i) * RPI + sub;
       const int hy = hr / HW, hx = hr - hy * HW;
-      const int ys = y0 + hy, xs = x0 + hx;
-      const bool ok = live && hr < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws;
+      int ys = y0 + hy, xs = x0 + hx, im = img;
+      if constexpr (IX > 1) {                         // image b, column hx - b (IW + 1) - 1 (-1: a pad)
+        const int b = min(hx / (IW + 1), IX - 1);
+        xs = hx - b * (IW + 1) - 1;
+        im = img + b;
+      }
+      const bool ok = live && hr < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < (IX > 1 ? IW : a.Ws);
       const uint32_t off =
-          ok ? (uint32_t)((((img * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hx, slot) * 8) * 2) : BAD;
+          ok ? (uint32_t)((((im * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hx, slot) * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs_src, (__attribute__((address_space(3))) void*)(st + (wave * HI + i) * RPI * 64), 16, off, 0, 0, 0);
     }
@@ -1013,7 +1036,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
     const int p = wave * WTM + i * 16 + fr;
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
-      const int hx = p % PW + dx;
+      const int px = p % PW, hx = px + px / IW * (IX > 1 ? 1 : 0) + dx;   // + one shared pad per image
       xb[i][dx] = ((p / PW) * HW + hx) * 64 + swzh(hx, fk) * 16;
     }
   }
@@ -1165,7 +1188,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       // exactly NSTORE = 2 * TM stores.  Sums: DPP reduce-scatter over the 16 pixels of a
       // fragment row, one LDS pass over the waves.
       const int nt = cit / ntiles, tile = cit - nt * ntiles;
-      const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
       const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
       const __amdgpu_buffer_rsrc_t rs_dst =
           __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
@@ -1175,8 +1198,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int p = wave * WTM + i * 16 + fr;
-        const int y = ty * PH + p / PW, x = tx * PW + p % PW;
-        mq[i] = (y < a.Hd && x < a.Wd) ? (img * a.Hd + y) * a.Wd + x : -1;
+        mq[i] = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           float f[8];
@@ -1214,10 +1236,9 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
         for (int k = 0; k < WTM / 8; ++k) {
           const int r = k * 8 + (lane >> 3), p = wave * WTM + r;       // 8 pixel rows per instruction
-          const int y = ty * PH + p / PW, x = tx * PW + p % PW;
+          const int m = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
           const int c = (lane & 7) ^ (r & 7);
-          const uint32_t off = (y < a.Hd && x < a.Wd)
-              ? (uint32_t)((((size_t)(img * a.Hd + y) * a.Wd + x) * a.bnr_ycs + nt * BN + c * 8) * 2) : 0xFFFFFFF0u;
+          const uint32_t off = m >= 0 ? (uint32_t)(((size_t)m * a.bnr_ycs + nt * BN + c * 8) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(
               rs_y, (__attribute__((address_space(3))) void*)(yl + k * 1024), 16, off, 0, 0, 0);
         }
@@ -1336,7 +1357,7 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       // BN partial sums from the stored values; raw barriers only, so nothing
       // drains the stores or the DMA already in flight.
       const int nt = cit / ntiles, tile = cit - nt * ntiles;
-      const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
       char* ot = smem + buf * STAGE;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();                     // every wave is done reading this stage
@@ -1364,9 +1385,9 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
 #pragma unroll
       for (int k = 0; k < NSTORE; ++k) {
         const int p = (tid >> 3) + PPP * k;
-        const int y = ty * PH + p / PW, x = tx * PW + p % PW;
-        const bool ok = y < a.Hd && x < a.Wd;
-        const int m = (img * a.Hd + y) * a.Wd + x;
+        const int mm = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
+        const bool ok = mm >= 0;
+        const int m = ok ? mm : 0;
         uint4 u = *reinterpret_cast<const uint4*>(ot + p * 128 + ((c16 ^ (p & 7)) << 4));
         const uint32_t off = ok ? (uint32_t)(((size_t)m * a.dcs + nt * BN + c16 * 8) * 2) : 0xFFFFFFF0u;
         float f[8];
@@ -1431,6 +1452,19 @@ __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_k
       for (int k = 0; k < 5; ++k) d[k] = tb[k];
     }
   }
+}
+
+template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT = 0, bool BNR = false>
+__global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes,
+                                                                                    int TY, int TX, int per, int rem) {
+  halo_body<PH, PW, NW, STAGES, DIAG, DIRECT, BNR, 1>(a, src_bytes, TY, TX, per, rem);
+}
+
+// two 16 x 16 images per 16 x 32 tile (IX = 2); TY = TX = 1
+template <int DIRECT, bool BNR>
+__global__ __launch_bounds__(512, 1) void conv3x3_halo2_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
+                                                               int rem) {
+  halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2>(a, src_bytes, TY, TX, per, rem);
 }
 
 constexpr int HALO_PW = 32;
@@ -1645,11 +1679,28 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
   tx = (c.Wd + halo_pw(c) - 1) / halo_pw(c);
 }
 
+// images per halo tile: 2 for 16 x 16 layers (conv3x3_halo2_kernel: two images side by side
+// in one 16 x 32 tile) when the statistics groups hold an even number of images.
+// STF_HALO2=0: one 16 x 16 image per tile; 1 (default): forward convs (with BN statistics)
+// only -- the dgrads run beside the side-stream weight gradients, and the 160 KiB workgroup
+// of the wide tile cannot share a CU with them (128 KiB for the 16 x 16 tile); 2: all
+int halo_ix(const stf_igemm_args* a) {
+  static const int mode = [] { const char* e = getenv("STF_HALO2"); return e ? atoi(e) : 1; }();
+  const stf_conv_geom& c = a->g;
+  if (mode == 0 || (mode == 1 && !a->stats)) return 1;
+  if (halo_variant() != 0 || c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
+  const long M = (long)c.N * c.Hd * c.Wd;
+  const long Mg = a->group_rows > 0 ? a->group_rows : M;
+  return ((Mg / (c.Hd * c.Wd)) % 2) ? 1 : 2;
+}
+
 // persistent halo grid: one workgroup per CU (160 KiB LDS each)
 int halo_grid(const stf_igemm_args* a) {
   int ty, tx;
   halo_tiles(a->g, ty, tx);
-  const long items = (long)a->g.N * ty * tx * (a->Nout / 64);
+  const int ix = halo_ix(a);
+  if (ix > 1) ty = tx = 1;
+  const long items = (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
   return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 ? 2 : 1));
 }
 
@@ -1716,7 +1767,10 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
     case 'H':
-      if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false>", HALO_PW);
+      if (halo_ix(a) > 1)
+        snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
+                 bnr_fused(a, k) ? "true" : "false");
+      else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false>", HALO_PW);
       else
         snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, %d, %s>", halo_pw(c),
                  halo_direct(a) ? (a->stats ? 2 : 1) : 0, bnr_fused(a, k) ? "true" : "false");
@@ -1810,7 +1864,9 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
     int ty, tx;
     halo_tiles(c, ty, tx);
-    const long items = (long)c.N * ty * tx * (a->Nout / 64);
+    const int ix = halo_ix(a);
+    if (ix > 1) ty = tx = 1;
+    const long items = (long)(c.N / ix) * ty * tx * (a->Nout / 64);
     const int grid = halo_grid(a);
     static const int diag = [] { const char* e = getenv("STF_HALO_DIAG"); return e ? atoi(e) : 0; }();
 #define STF_H(D) do {                                                                                            \
@@ -1825,7 +1881,14 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     const int per = (int)(items / grid), rem = (int)(items % grid);
 #define STF_HL(PWV, D, B) hipLaunchKernelGGL((conv3x3_halo_kernel<16, PWV, 8, 2, 0, D, B>), dim3(grid), dim3(512), 0, \
                                              s, g, src_bytes, ty, tx, per, rem)
-    if (bnr_fused(a, k)) {
+#define STF_H2(D, B) hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B>), dim3(grid), dim3(512), 0, s, g, src_bytes, \
+                                        ty, tx, per, rem)
+    if (ix > 1) {
+      if (bnr_fused(a, k)) STF_H2(1, true);
+      else if (d == 2) STF_H2(2, false);
+      else if (d == 1) STF_H2(1, false);
+      else STF_H2(0, false);
+    } else if (bnr_fused(a, k)) {
       if (halo_pw(c) == 16) STF_HL(16, 1, true);
       else STF_HL(HALO_PW, 1, true);
     } else if (halo_pw(c) == 16) {
@@ -1844,6 +1907,7 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     } else if (d == 2) STF_HL(HALO_PW, 2, false);
     else if (d == 1) STF_HL(HALO_PW, 1, false);
     else STF_H(0);
+#undef STF_H2
 #undef STF_HL
 #undef STF_H
     STF_CHECK_LAUNCH();

@@ -140,6 +140,8 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     (1, 96, 64, 64, 80, 1, False, 96, 0),        # three chunks
     (4, 64, 128, 16, 16, 2, False, 64, 0),       # 16x16 tiles (16 <= W < 32), grouped statistics
     (2, 128, 64, 21, 24, 1, True, 128, 0),       # 16x16 tiles, ragged, accumulate
+    (6, 256, 256, 16, 16, 3, True, 320, 64),     # two 16x16 images per 16x32 tile, accumulate, slice source
+    (3, 64, 64, 16, 16, 3, False, 64, 0),        # one image per group: single-image 16x16 tiles
 ])
 def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
@@ -209,6 +211,7 @@ def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
 @pytest.mark.parametrize("n,cin,cout,H,W,groups,relu,acc", [
     (2, 64, 128, 40, 72, 1, True, False),     # halo 16x32 tiles, ragged edges
     (4, 128, 64, 24, 20, 2, True, False),     # halo 16x16 tiles, two BN groups
+    (8, 256, 256, 16, 16, 2, True, False),    # two 16x16 images per halo tile (STF layer3)
     (2, 64, 64, 64, 64, 1, False, True),      # plain BN (no ReLU), accumulate
     (4, 256, 128, 8, 8, 2, True, False),      # linear kernel: separate reduce fallback
 ])
