@@ -119,8 +119,10 @@ __global__ void pack_weights_kernel(const stf_pack_desc* __restrict__ descs) {
 // tiles through LDS; modes whose rows run along b (0: [co][tap][ci(pad)], 3: [ci][tap]
 // [co]) transpose per-a [b][tap] blocks (4 a x 64 b).  Reads are whole source rows,
 // writes are 16-B chunks of output rows (the element-wise gather above reads one
-// scattered float per output: ~1.3 TB/s effective, 0.28 ms per cfg2 step).
-constexpr int PK_TA = 64, PK_TB = 16, PK_IA = 4, PK_IB = 64, PK_MAXRS = 9;
+// scattered float per output: ~1.3 TB/s effective, 0.28 ms per cfg2 step).  32-row A tiles: 18.6 KB
+// of LDS, 8 blocks per CU (64-row tiles, 37 KB, allowed 4: cfg2 167 -> 115 us per step, STF cfg3
+// 127 -> 94 us; 16-row tiles 123 / 96 us).
+constexpr int PK_TA = 32, PK_TB = 16, PK_IA = 4, PK_IB = 64, PK_MAXRS = 9;
 
 STF_DEV bool pack_outer(int mode) { return mode == 1 || mode == 5 || mode == 2 || mode == 4; }
 
