@@ -115,7 +115,7 @@ __global__ void pack_weights_kernel(const stf_pack_desc* __restrict__ descs) {
 
 // Tiled packing (every descriptor of the list in one launch; blockIdx.y = descriptor).
 // Source w is [A = d0][Bc = d1][RS] fp32.  Modes whose rows run along A (1, 5: Conv
-// dgrad rows [ci][tap][co]; 2, 4: ConvT rows over ci) transpose 64 (a) x 16 (b) x RS
+// dgrad rows [ci][tap][co]; 2, 4: ConvT rows over ci) transpose 32 (a) x 16 (b) x RS
 // tiles through LDS; modes whose rows run along b (0: [co][tap][ci(pad)], 3: [ci][tap]
 // [co]) transpose per-a [b][tap] blocks (4 a x 64 b).  Reads are whole source rows,
 // writes are 16-B chunks of output rows (the element-wise gather above reads one
