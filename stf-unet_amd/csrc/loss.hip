@@ -39,26 +39,27 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
   // CG lanes of one pixel are adjacent (NT and the grid stride are multiples of
   // CG, so a thread's channel group is fixed); 4 pixels per thread per round so
   // four 16-B loads are in flight before any arithmetic
+  // 32-bit index math (the host checks P * CG < 2^31): 64-bit divisions cost ~40 instructions
   constexpr int U = 4;
   const int CG = C / 8;
-  const long units = P * CG;
-  const int cg = (int)((blockIdx.x * (long)NT + threadIdx.x) % CG);
+  const int units = (int)(P * CG);
+  const int cg = (int)((blockIdx.x * NT + threadIdx.x) % CG);
   float sc[8], sh[8], wk[K][8], bk[K];
   load8f(scale + cg * 8, sc);
   load8f(shift + cg * 8, sh);
 #pragma unroll
   for (int k = 0; k < K; ++k) { load8f(w + k * C + cg * 8, wk[k]); bk[k] = bias[k]; }
-  const long stride = (long)gridDim.x * NT;
-  for (long u0 = blockIdx.x * (long)NT; u0 < units; u0 += stride * U) {
+  const int stride = gridDim.x * NT;
+  for (int u0 = blockIdx.x * NT; u0 < units; u0 += stride * U) {
     uint4 raw[U];
 #pragma unroll
     for (int r = 0; r < U; ++r) {
-      const long u = u0 + r * stride + threadIdx.x;
-      raw[r] = u < units ? *reinterpret_cast<const uint4*>(y + (u / CG) * C + cg * 8) : make_uint4(0, 0, 0, 0);
+      const int u = u0 + r * stride + threadIdx.x;
+      raw[r] = u < units ? *reinterpret_cast<const uint4*>(y + (size_t)(u / CG) * C + cg * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < U; ++r) {
-      const long u = u0 + r * stride + threadIdx.x;
+      const int u = u0 + r * stride + threadIdx.x;
       float v[8], acc[K];
       unpack8(raw[r], v);
 #pragma unroll
@@ -73,9 +74,9 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
       for (int k = 0; k < K; ++k)
         for (int o = 1; o < CG; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
       if (u < units && cg == 0) {
-        const long pix = u / CG, n = pix / HW, hw = pix - n * HW;
+        const int pix = u / CG, n = pix / HW, hw = pix - n * HW;
 #pragma unroll
-        for (int k = 0; k < K; ++k) logits[(n * K + k) * HW + hw] = acc[k] + bk[k];
+        for (int k = 0; k < K; ++k) logits[(size_t)(n * K + k) * HW + hw] = acc[k] + bk[k];
       }
     }
   }
@@ -90,9 +91,9 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_
   constexpr int NV = 16 + 8 * K + K;       // sg[8], sgx[8], dW[K][8], db[K]
   __shared__ float red[NT][NV + 1];
   const int CG = C / 8;
-  const long units = P * CG;
-  const long gt = blockIdx.x * (long)NT + threadIdx.x;
-  const int cg = (int)(gt % CG);
+  const int units = (int)(P * CG);                // < 2^31 (host check): 32-bit index math
+  const int gt = blockIdx.x * NT + threadIdx.x;
+  const int cg = gt % CG;
   float sc[8], sh[8], mu[8], is[8], wk[K][8];
   load8f(scale + cg * 8, sc);
   load8f(shift + cg * 8, sh);
@@ -107,14 +108,30 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_
 #pragma unroll
     for (int j = 0; j < 8; ++j) dw[k][j] = 0.f;
   }
-  for (long u = gt; u < units; u += (long)gridDim.x * NT) {
-    const long pix = u / CG;
-    const long n = pix / HW, hw = pix - n * HW;
-    float dl[K];
+  // one unit per iteration (two with the loads hoisted: 219 -> 245 us at cfg2, fewer waves)
+  constexpr int U = 1;
+  const int S = gridDim.x * NT;
+  for (int u0 = gt; u0 < units; u0 += S * U) {
+    float dlr[U][K];
+    uint4 yr[U];
+    int pixr[U];
 #pragma unroll
-    for (int k = 0; k < K; ++k) dl[k] = dlogits[(n * K + k) * HW + hw];
+    for (int r = 0; r < U; ++r) {
+      const int u = u0 + r * S;
+      const bool ok = u < units;
+      const int pix = ok ? u / CG : 0, n = pix / HW, hw = pix - n * HW;
+      pixr[r] = ok ? pix : -1;
+#pragma unroll
+      for (int k = 0; k < K; ++k) dlr[r][k] = ok ? dlogits[(size_t)(n * K + k) * HW + hw] : 0.f;
+      yr[r] = ok ? *reinterpret_cast<const uint4*>(y + (size_t)pix * C + cg * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+    if (pixr[r] < 0) continue;
+    const int pix = pixr[r];
+    const float* dl = dlr[r];
     float v[8], g[8];
-    unpack8(*reinterpret_cast<const uint4*>(y + pix * C + cg * 8), v);
+    unpack8(yr[r], v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float z = v[j] * sc[j] + sh[j];
@@ -130,7 +147,8 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_
 #pragma unroll
       for (int k = 0; k < K; ++k) db[k] += dl[k];
     }
-    *reinterpret_cast<uint4*>(g_out + pix * C + cg * 8) = pack8(g);
+    *reinterpret_cast<uint4*>(g_out + (size_t)pix * C + cg * 8) = pack8(g);
+    }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = sg[j]; red[threadIdx.x][8 + j] = sgx[j]; }
@@ -284,12 +302,15 @@ __global__ void loss_bwd_kernel(const float* __restrict__ logits, const int64_t*
   }
 }
 
-__global__ void sum_tiles_kernel(const float* __restrict__ partial, int tiles, int C, float* __restrict__ out) {
+// column sums of partial[tiles][C]: columns < split go to out[c], the rest to out2[c - split]
+__global__ void sum_tiles_kernel(const float* __restrict__ partial, int tiles, int C, int split,
+                                 float* __restrict__ out, float* __restrict__ out2) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s = 0.0;
   for (int t = 0; t < tiles; ++t) s += partial[(size_t)t * C + c];
-  out[c] = (float)s;
+  if (c < split) out[c] = (float)s;
+  else out2[c - split] = (float)s;
 }
 
 bool head_ok(int C) { return C % 8 == 0 && C / 8 <= 64 && 64 % (C / 8) == 0; }
@@ -311,6 +332,7 @@ extern "C" int stf_head_fwd(const void* y, int N, int H, int W, int C, const flo
                             const float* w, const float* bias, int classes, float* logits, stf_stream_t stream) {
   if (!head_ok(C)) return STF_EINVAL;
   const long P = (long)N * H * W, units = P * (C / 8);
+  if (units >= (1L << 31)) return STF_EINVAL;
   long blocks = (units + NT - 1) / NT;
   if (blocks > 8192) blocks = 8192;
   hipStream_t s = (hipStream_t)stream;
@@ -324,7 +346,7 @@ extern "C" int stf_head_bwd(const float* dlogits, const void* y, int N, int H, i
                             const float* shift, const float* mean, const float* invstd, const float* w, int classes,
                             void* g_out, float* bn_partial, float* head_partial, float* dw, float* db,
                             stf_stream_t stream) {
-  if (!head_ok(C)) return STF_EINVAL;
+  if (!head_ok(C) || (long)N * H * W * (C / 8) >= (1L << 31)) return STF_EINVAL;
   const long P = (long)N * H * W;
   const int tiles = stf_head_tiles(N, H, W, C);
   hipStream_t s = (hipStream_t)stream;
@@ -333,17 +355,12 @@ extern "C" int stf_head_bwd(const float* dlogits, const void* y, int N, int H, i
                                             (uint16_t*)g_out, bn_partial, head_partial));
   STF_CHECK_LAUNCH();
   const int HC = classes * (C + 1);
-  // reduce [tiles][K*(C+1)] into row `tiles` of the slab, then split into dw[K*C], db[K]
+  // reduce [tiles][K*(C+1)] straight into dw[K*C] and db[K]
   const int S = stf::colsum_stage1(head_partial, tiles, HC, s);
-  hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, S, HC,
-                     head_partial + (size_t)tiles * HC);
+  hipLaunchKernelGGL(sum_tiles_kernel, dim3((HC + 255) / 256), dim3(256), 0, s, head_partial, S, HC, classes * C,
+                     dw, db);
   STF_CHECK_LAUNCH();
-  hipError_t e = stf::memcpy_async(dw, head_partial + (size_t)tiles * HC, sizeof(float) * classes * C,
-                                hipMemcpyDeviceToDevice, s);
-  if (e == hipSuccess)
-    e = stf::memcpy_async(db, head_partial + (size_t)tiles * HC + classes * C, sizeof(float) * classes,
-                       hipMemcpyDeviceToDevice, s);
-  return (int)e;
+  return 0;
 }
 
 extern "C" int stf_loss_scratch_floats(int N, int classes) {
