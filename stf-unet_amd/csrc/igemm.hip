@@ -1684,10 +1684,12 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
 // STF_HALO2=0: one 16 x 16 image per tile; 1 (default): forward convs (with BN statistics)
 // only -- the dgrads run beside the side-stream weight gradients, and the 160 KiB workgroup
 // of the wide tile cannot share a CU with them (128 KiB for the 16 x 16 tile); 2: all
-int halo_ix(const stf_igemm_args* a) {
+// with_stats: the launch writes BN statistics (the size queries pass what the launch will do:
+// stf_igemm_stat_tiles is asked before the statistics buffer exists)
+int halo_ix(const stf_igemm_args* a, bool with_stats) {
   static const int mode = [] { const char* e = getenv("STF_HALO2"); return e ? atoi(e) : 1; }();
   const stf_conv_geom& c = a->g;
-  if (mode == 0 || (mode == 1 && !a->stats)) return 1;
+  if (mode == 0 || (mode == 1 && !with_stats)) return 1;
   if (halo_variant() != 0 || c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
@@ -1695,10 +1697,9 @@ int halo_ix(const stf_igemm_args* a) {
 }
 
 // persistent halo grid: one workgroup per CU (160 KiB LDS each)
-int halo_grid(const stf_igemm_args* a) {
+int halo_grid(const stf_igemm_args* a, int ix) {
   int ty, tx;
   halo_tiles(a->g, ty, tx);
-  const int ix = halo_ix(a);
   if (ix > 1) ty = tx = 1;
   const long items = (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
   return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 ? 2 : 1));
@@ -1732,7 +1733,7 @@ int stat_tiles(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
-  if (choose(a, dma_fits(a)) == 'H') return halo_grid(a);
+  if (choose(a, dma_fits(a)) == 'H') return halo_grid(a, halo_ix(a, true));
   if (ksplit_of(a) > 1) return (int)((Mg + sk_rows(a->Nout) - 1) / sk_rows(a->Nout));
   const int bm = pick_mtile(a);
   return (int)((Mg + bm - 1) / bm);
@@ -1753,7 +1754,7 @@ extern "C" int stf_igemm_bnr_tiles(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
   const long M = (long)c.N * c.Hd * c.Wd;
   const int groups = a->group_rows > 0 ? (int)(M / a->group_rows) : 1;
-  if (bnr_fused(a, choose(a, dma_fits(a)))) return halo_grid(a);
+  if (bnr_fused(a, choose(a, dma_fits(a)))) return halo_grid(a, halo_ix(a, false));
   return stf_bn_bwd_tiles(c.N, c.Hd, c.Wd, a->Nout, groups, 0);
 }
 
@@ -1767,7 +1768,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
     case 'H':
-      if (halo_ix(a) > 1)
+      if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false");
       else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false>", HALO_PW);
@@ -1864,10 +1865,10 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
     int ty, tx;
     halo_tiles(c, ty, tx);
-    const int ix = halo_ix(a);
+    const int ix = halo_ix(a, a->stats != nullptr);
     if (ix > 1) ty = tx = 1;
     const long items = (long)(c.N / ix) * ty * tx * (a->Nout / 64);
-    const int grid = halo_grid(a);
+    const int grid = halo_grid(a, ix);
     static const int diag = [] { const char* e = getenv("STF_HALO_DIAG"); return e ? atoi(e) : 0; }();
 #define STF_H(D) do {                                                                                            \
     if (halo_variant() == 1)                                                                                     \

@@ -28,7 +28,9 @@ are overwritten by the next step's forward.
 ``STF_PLAN=0`` keeps every step eager (A/B, debugging); ``STF_PLAN_WARM`` sets the
 number of eager steps before recording (default 1).
 """
+import contextlib
 import ctypes
+import gc
 import os
 import weakref
 from collections import OrderedDict
@@ -86,6 +88,21 @@ class Plan:
         h, self.h = getattr(self, "h", None), None
         if h:
             self.lib.stf_plan_destroy(h)
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """No cyclic garbage collection while a recording allocates from a private pool: a
+    collected MemPool (an evicted entry's, or a dead program's) empties its cache on
+    destruction, which torch refuses while any pool context is active -- a C++ exception
+    inside a destructor, i.e. an abort."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _pool_ctx():
@@ -191,6 +208,10 @@ class StepRuntime:
         return e.logits, e.S
 
     def _record_forward(self, e, x, training):
+        with _no_gc():
+            self._record_forward_pooled(e, x, training)
+
+    def _record_forward_pooled(self, e, x, training):
         pool, ctx = _pool_ctx()
         e.pool = pool
         nhwc.KEEP = e.keep
@@ -228,6 +249,10 @@ class StepRuntime:
         e.bwd.replay(pos)
 
     def _record_backward(self, e, S, dlogits, bsig):
+        with _no_gc():
+            self._record_backward_pooled(e, S, dlogits, bsig)
+
+    def _record_backward_pooled(self, e, S, dlogits, bsig):
         p = self.prog
         e.bwd = None
         e.bkeep = []

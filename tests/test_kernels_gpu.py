@@ -147,6 +147,9 @@ def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
     BN partial statistics, accumulate, and the stride-1 dgrad over flipped taps."""
     from stfunet import nhwc
+    # NaN-filled blocks back in the caching allocator: a statistics row the kernel does not
+    # write (a grid that disagrees with stf_igemm_stat_tiles) shows up as NaN below
+    torch.full((16 << 20,), float("nan"), device=DEV)
     x = bfr(torch.randn(n, cin, H, W, device=DEV))
     w = bfr(torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5)
     b = torch.randn(cout, device=DEV)

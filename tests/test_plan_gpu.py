@@ -205,3 +205,38 @@ def test_plan_utility_ops():
         b = a * 2
     nhwc.wait(torch.cuda.current_stream(), side)
     assert bool((b == 2).all())
+
+
+_GC_SCRIPT = r"""
+import gc, sys, torch
+sys.path.insert(0, "stf-unet_amd")
+from stfunet import UNet, engine
+from stfunet.synthetic import dce_batch
+x, t = dce_batch(2, 8, 64, 64, seed=0, device="cuda")
+x = x.flatten(1, 2)
+def steps(m):
+    for _ in range(3):
+        engine.criterion(m(x), t).backward()
+a = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
+steps(a)                        # a's plans and private pool are recorded
+a.cycle = a                     # only the cyclic collector can free a (and its pool) now
+del a
+gc.set_threshold(1, 1, 1)       # collect at (nearly) every allocation
+b = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
+steps(b)                        # b records while a is garbage
+gc.collect()
+torch.cuda.synchronize()
+print("ok")
+"""
+
+
+def test_plan_recording_survives_collection_of_a_dead_programs_pool():
+    """A dead program's private memory pool collected by the cyclic GC in the middle of
+    another program's recording aborted the process (the pool's destructor empties its
+    cache, which torch refuses while a pool context is active); recordings run with the
+    cyclic collector off.  In a child process: a regression here is an abort."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _GC_SCRIPT], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stderr[-3000:])
