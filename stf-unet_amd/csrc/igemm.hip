@@ -1467,6 +1467,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo2_kernel(Geo a, uint32_t s
   halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2>(a, src_bytes, TY, TX, per, rem);
 }
 
+// four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves, one stage, two workgroups
+// per CU (61 KB of LDS each)
+template <int DIRECT>
+__global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
+                                                               int rem) {
+  halo_body<8, 32, 4, 1, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
+}
+
 constexpr int HALO_PW = 32;
 // variant: 0 = 16x32 tile, 8 waves, 2-stage ring (1 WG/CU); 1 = 8x32, 4 waves, 1 stage (2 WG/CU)
 int halo_variant() {
@@ -1490,11 +1498,23 @@ long halo_items(const stf_conv_geom& c, int nout) {
   const long ty = (c.Hd + halo_ph() - 1) / halo_ph(), tx = (c.Wd + halo_pw(c) - 1) / halo_pw(c);
   return (long)c.N * ty * tx * (nout / 64);
 }
+// 8 x 8 layers through the halo kernel, four images per 8 x 32 tile (conv3x3_halo4_kernel;
+// STF_HALO4=0: the linear split-K kernels, A/B)
+bool halo8(const stf_igemm_args* a) {
+  static const int mode = [] { const char* e = getenv("STF_HALO4"); return e ? atoi(e) : 1; }();
+  const stf_conv_geom& c = a->g;
+  if (mode == 0 || (mode == 2 && a->bnr)) return false;
+  if (halo_variant() != 0 || c.Hd != 8 || c.Wd != 8 || c.N % 4 || a->Nout % 64 || c.Cs % 32) return false;
+  const long M = (long)c.N * c.Hd * c.Wd;
+  const long Mg = a->group_rows > 0 ? a->group_rows : M;
+  return (Mg / (c.Hd * c.Wd)) % 4 == 0;
+}
+
 // direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad),
 // =2 always (default: measured 1.7 % faster on the forward convs than the LDS-staged one)
 bool halo_direct(const stf_igemm_args* a) {
   static const int mode = [] { const char* e = getenv("STF_HALO_DIRECT"); return e ? atoi(e) : 2; }();
-  return halo_variant() == 0 && (mode == 2 || (mode == 1 && !a->stats));
+  return halo_variant() == 0 && !halo8(a) && (mode == 2 || (mode == 1 && !a->stats));
 }
 
 // BN-backward reduction fused into the halo direct epilogue (STF_BNR_FUSED=0: separate
@@ -1576,6 +1596,7 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= halo_min_w() && a->Nout <= 256)) &&
       halo_items(c, a->Nout) >= halo_min_items())
     return 'H';
+  if (f == '0' && halo_ok && halo8(a)) return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
     if ((plain || a->scatter2x2) && bk64 && !a->lstm && !c.transposed) return f;
@@ -1689,6 +1710,7 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
 int halo_ix(const stf_igemm_args* a, bool with_stats) {
   static const int mode = [] { const char* e = getenv("STF_HALO2"); return e ? atoi(e) : 1; }();
   const stf_conv_geom& c = a->g;
+  if (halo8(a)) return 4;
   if (mode == 0 || (mode == 1 && !with_stats)) return 1;
   if (halo_variant() != 0 || c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
   const long M = (long)c.N * c.Hd * c.Wd;
@@ -1702,7 +1724,7 @@ int halo_grid(const stf_igemm_args* a, int ix) {
   halo_tiles(a->g, ty, tx);
   if (ix > 1) ty = tx = 1;
   const long items = (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
-  return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 ? 2 : 1));
+  return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 || ix == 4 ? 2 : 1));
 }
 
 // Split-K factor for a plain gather on the linear DMA kernels that would leave the
@@ -1768,7 +1790,9 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
     case 'H':
-      if (halo_ix(a, a->stats != nullptr) > 1)
+      if (halo8(a))
+        snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
+      else if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false");
       else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false>", HALO_PW);
@@ -1884,7 +1908,9 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
                                              s, g, src_bytes, ty, tx, per, rem)
 #define STF_H2(D, B) hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B>), dim3(grid), dim3(512), 0, s, g, src_bytes, \
                                         ty, tx, per, rem)
-    if (ix > 1) {
+    if (ix == 4) {
+      hipLaunchKernelGGL((conv3x3_halo4_kernel<0>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
+    } else if (ix > 1) {
       if (bnr_fused(a, k)) STF_H2(1, true);
       else if (d == 2) STF_H2(2, false);
       else if (d == 1) STF_H2(1, false);

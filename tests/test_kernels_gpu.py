@@ -142,6 +142,8 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     (2, 128, 64, 21, 24, 1, True, 128, 0),       # 16x16 tiles, ragged, accumulate
     (6, 256, 256, 16, 16, 3, True, 320, 64),     # two 16x16 images per 16x32 tile, accumulate, slice source
     (3, 64, 64, 16, 16, 3, False, 64, 0),        # one image per group: single-image 16x16 tiles
+    (16, 512, 512, 8, 8, 4, False, 512, 0),      # four 8x8 images per 8x32 tile (STF layer4)
+    (8, 256, 128, 8, 8, 2, True, 320, 64),       # 8x8 four-image tiles, accumulate, slice source
 ])
 def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
@@ -199,6 +201,7 @@ def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
         ref = ref + base
     src = feat_from(x)
     a = _lib.IgemmArgs(nhwc._geom(src, H, W, R, R, 1, pad, False), src.ptr(), None, cout, dst.ptr(), cout)
+    a.group_rows = n * H * W // groups
     assert _lib.load().stf_igemm_ws_bytes(ctypes.byref(a)) > 0, "shape expected to run split over K"
     stats, tiles = nhwc.igemm(src, nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst, R, R, 1, pad, bias=b,
                               want_stats=True, groups=groups, accumulate=acc)
@@ -216,7 +219,8 @@ def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
     (4, 128, 64, 24, 20, 2, True, False),     # halo 16x16 tiles, two BN groups
     (8, 256, 256, 16, 16, 2, True, False),    # two 16x16 images per halo tile (STF layer3)
     (2, 64, 64, 64, 64, 1, False, True),      # plain BN (no ReLU), accumulate
-    (4, 256, 128, 8, 8, 2, True, False),      # linear kernel: separate reduce fallback
+    (6, 256, 128, 8, 8, 2, True, False),      # linear kernel (6 images: no 4-image halo tiles): separate reduce
+    (8, 256, 128, 8, 8, 2, True, False),      # 8x8 four-image halo tiles: separate reduce
 ])
 def test_dgrad_fused_bn_backward_reduce(n, cin, cout, H, W, groups, relu, acc):
     """conv_dgrad with ``bnr``: dz identical to the plain dgrad, and the fused partial
