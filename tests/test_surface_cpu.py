@@ -174,6 +174,34 @@ def test_size_queries_depend_only_on_the_cached_signature():
         assert len(res) == 1, (N, Hs, Cs, nout, res)
 
 
+def test_stat_tile_query_does_not_depend_on_the_stats_pointer():
+    """Callers ask stf_igemm_stat_tiles BEFORE the statistics buffer exists (its size is the
+    answer), so the answer -- and the kernel the launch will pick -- must not change once the
+    pointer is set; a multi-image halo path chosen only with stats set once left rows of the
+    buffer unwritten (host-only calls, no GPU)."""
+    from stfunet import _lib
+    lib = _lib.load()
+    shapes = [  # N, H, W, Cs, Nout, groups
+        (128, 16, 16, 256, 256, 8),     # STF layer3: two images per 16x32 halo tile
+        (4, 16, 16, 64, 128, 2),        # even images per group
+        (3, 16, 16, 64, 64, 3),         # one image per group
+        (128, 8, 8, 512, 512, 8),       # STF layer4: four images per 8x32 tile
+        (8, 8, 8, 256, 128, 2),
+        (6, 8, 8, 256, 128, 2),         # not a multiple of four images
+        (64, 256, 256, 64, 64, 1),
+        (64, 32, 32, 512, 512, 1),
+    ]
+    for N, H, W, Cs, nout, groups in shapes:
+        M = N * H * W
+        g = _lib.ConvGeom(N, H, W, Cs, Cs, H, W, 3, 3, 1, 1, 0)
+        a = _lib.IgemmArgs(g, 1 << 32, 2 << 32, nout, 3 << 32, nout, None, None, 0,
+                           M // groups if groups > 1 else 0, 0, None)
+        before = (lib.stf_igemm_stat_tiles(ctypes.byref(a)), lib.stf_igemm_ws_bytes(ctypes.byref(a)))
+        a.stats = 4 << 32
+        after = (lib.stf_igemm_stat_tiles(ctypes.byref(a)), lib.stf_igemm_ws_bytes(ctypes.byref(a)))
+        assert before[0] == after[0], (N, H, Cs, nout, groups, before, after)
+
+
 def _ref_keys():
     import json
     with open(os.path.join(GOLDEN, "state_dict_keys.json")) as f:
