@@ -1475,6 +1475,165 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t s
   halo_body<8, 32, 4, 1, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 convolution of an 8-channel input (UNet's first layer: in_channels = 8,
+// src/unet.py:12): K = 9 taps x 8 channels = 72, three 32-deep MFMA steps (taps 9-11 zero).  A
+// workgroup walks 16 x 16 pixel tiles; per tile the 18 x 18 halo of 16-B rows (one pixel's 8
+// channels) is staged in LDS once, and every MFMA B fragment -- 8 channels of one pixel at one tap
+// -- is ONE ds_read_b128 of halo row (pixel + tap offset).  The 64 x 72 weights stay in registers
+// for the whole launch.  (The linear kernel gathers the 16-B row of every tap with its own LDS-DMA
+// instruction: ~9x the issue work for the same bytes.)  Weight rows are permuted as in the halo
+// kernel's DIRECT epilogue, so each lane stores 16-B chunks of 8 consecutive channels straight
+// from its accumulators; BN partial sums per (statistics group, workgroup) from the stored values.
+constexpr int C8_T = 16, C8_HW = C8_T + 2, C8_HR = C8_HW * C8_HW;      // 324 halo rows per tile
+__global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int TX, int per, int rem) {
+  __shared__ __attribute__((aligned(16))) uint4 halo[2][C8_HR];
+  __shared__ float red[4][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int tpi = TY * TX;
+  const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
+  const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  const int ipg = a.Mg / (a.Hd * a.Wd), groups = a.M / a.Mg;
+  // weights: A row m of fragment j = output channel (j >> 1) * 32 + (m >> 2) * 8 + (j & 1) * 4 + (m & 3);
+  // lane (fr, fk) of k-step ks holds tap ks * 4 + fk (8 channels)
+  e16x8 wf[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = (j >> 1) * 32 + (fr >> 2) * 8 + (j & 1) * 4 + (fr & 3);
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int t = ks * 4 + fk;
+      wf[j][ks] = t < 9 ? *reinterpret_cast<const e16x8*>(a.wgt + (size_t)n * a.K + t * 8) : e16x8{};
+    }
+  }
+  // this lane's 16 accumulator channels: h * 32 + fk * 8 + e (e = (j & 1) * 4 + r, h = j >> 1)
+  float bv[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[h][e] = a.bias ? a.bias[h * 32 + fk * 8 + e] : 0.f;
+  if (a.stats && tid < 128) {           // this workgroup's rows of every group (the fold reads them all)
+    for (int g = 0; g < groups; ++g) a.stats[((size_t)(g * gridDim.x + blockIdx.x) * 2 + (tid >> 6)) * 64 + (tid & 63)] = 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t rs_dst =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, (uint32_t)((size_t)a.M * a.dcs * 2), 0x00020000);
+  uint4 ld[2];
+  auto load = [&](int tile) {
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int hr = tid + q * 256, hy = hr / C8_HW, hx = hr - hy * C8_HW;
+      const int ys = ty * C8_T - 1 + hy, xs = tx * C8_T - 1 + hx;
+      ld[q] = make_uint4(0, 0, 0, 0);
+      if (hr < C8_HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws)
+        ld[q] = *reinterpret_cast<const uint4*>(a.src + ((size_t)(img * a.Hs + ys) * a.Ws + xs) * a.scs);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (tid + q * 256 < C8_HR) halo[buf][tid + q * 256] = ld[q];
+  };
+  float s1[2][8], s2[2][8];
+  auto zero_sums = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[h][e] = 0.f; s2[h][e] = 0.f; }
+  };
+  int run_key = -1;
+  // the sums of the tiles since the last flush into this workgroup's row of group run_key
+  auto flush = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[h][e] += __shfl_xor(s1[h][e], o, 64);
+          s2[h][e] += __shfl_xor(s2[h][e], o, 64);
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wave][0][h * 32 + fk * 8 + e] = s1[h][e];
+          red[wave][1][h * 32 + fk * 8 + e] = s2[h][e];
+        }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int q = tid >> 6, c = tid & 63;
+      a.stats[((size_t)(run_key * gridDim.x + blockIdx.x) * 2 + q) * 64 + c] =
+          red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+    }
+    __syncthreads();
+    zero_sums();
+  };
+  zero_sums();
+  load(t0);
+  store(0);
+  __syncthreads();
+  for (int k = 0; k < cnt; ++k) {
+    const int tile = t0 + k, buf = k & 1;
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    if (k + 1 < cnt) load(tile + 1);
+    const int key = img / ipg;
+    if (a.stats && key != run_key) {
+      if (run_key >= 0) flush();
+      run_key = key;
+    }
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int t = ks * 4 + fk, dy = t / 3, dx = t - dy * 3;
+      e16x8 xf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 v = t < 9 ? halo[buf][(wave * 4 + i + dy) * C8_HW + fr + dx] : make_uint4(0, 0, 0, 0);
+        xf[i] = __builtin_bit_cast(e16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(wf[j][ks], xf[i], acc[i][j]);
+    }
+    // epilogue: pixel (row wave * 4 + i, column fr) of the tile; two 16-B stores per pixel
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int y = ty * C8_T + wave * 4 + i, x = tx * C8_T + fr;
+      const bool ok = y < a.Hd && x < a.Wd;
+      const size_t m = ((size_t)img * a.Hd + y) * a.Wd + x;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = round_e(acc[i][2 * h][r] + bv[h][r]);
+          f[4 + r] = round_e(acc[i][2 * h + 1][r] + bv[h][4 + r]);
+        }
+        const uint4 u = pack8(f);
+        const uint32_t off = ok ? (uint32_t)((m * a.dcs + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        if (ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[h][e] += f[e]; s2[h][e] += f[e] * f[e]; }
+        }
+      }
+    }
+    if (k + 1 < cnt) store(buf ^ 1);
+    __syncthreads();
+  }
+  if (a.stats && run_key >= 0) flush();
+}
+
 constexpr int HALO_PW = 32;
 // variant: 0 = 16x32 tile, 8 waves, 2-stage ring (1 WG/CU); 1 = 8x32, 4 waves, 1 stage (2 WG/CU)
 int halo_variant() {
@@ -1510,6 +1669,16 @@ bool halo8(const stf_igemm_args* a) {
   return (Mg / (c.Hd * c.Wd)) % 4 == 0;
 }
 
+// 8-channel-input 3x3 layer through conv3x3_c8_kernel (STF_C8HALO=0: the linear 'e' kernel, A/B)
+bool c8_halo(const stf_igemm_args* a) {
+  static const bool on = [] { const char* e = getenv("STF_C8HALO"); return !(e && e[0] == '0'); }();
+  const stf_conv_geom& c = a->g;
+  return on && !a->lstm && !a->scatter2x2 && !c.transposed && !a->bnr && !a->accumulate && c.Cs == 8 &&
+         c.src_cstride % 8 == 0 && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs &&
+         c.Wd == c.Ws && a->Nout == 64 && a->dst_cstride % 8 == 0 && ((uintptr_t)a->dst & 15) == 0 &&
+         (uint64_t)c.N * c.Hd * c.Wd * a->dst_cstride * 2 < 0xFFFFFF00ull;
+}
+
 // direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad),
 // =2 always (default: measured 1.7 % faster on the forward convs than the LDS-staged one)
 bool halo_direct(const stf_igemm_args* a) {
@@ -1533,6 +1702,9 @@ int num_cus() {
   }();
   return n;
 }
+
+int c8_tiles(const stf_conv_geom& c) { return c.N * ((c.Hd + C8_T - 1) / C8_T) * ((c.Wd + C8_T - 1) / C8_T); }
+int c8_grid(const stf_igemm_args* a) { return std::min(c8_tiles(a->g), 2 * num_cus()); }
 
 // Tile configurations of the DMA kernel.  'auto' picks per shape; the
 // STF_IGEMM_CFG environment variable forces one (A/B measurements).
@@ -1572,6 +1744,7 @@ bool dma_enabled() {
 char choose(const stf_igemm_args* a, bool dma_ok) {
   const stf_conv_geom& c = a->g;
   const bool plain = !a->lstm && !a->scatter2x2 && !c.transposed;
+  if (c8_halo(a) && forced_cfg() == '0') return 'K';     // 8-channel network input, 3x3
   if (dma_enabled() && dma_ok && plain && c.Cs == 8 && forced_cfg() != 'R')   // 8-channel network inputs
     return a->Nout <= 64 ? 'e' : 'a';
   if (!dma_enabled() || !dma_ok || c.Cs % 32) return 'R';
@@ -1756,6 +1929,7 @@ int stat_tiles(const stf_igemm_args* a) {
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
   if (choose(a, dma_fits(a)) == 'H') return halo_grid(a, halo_ix(a, true));
+  if (choose(a, dma_fits(a)) == 'K') return c8_grid(a);
   if (ksplit_of(a) > 1) return (int)((Mg + sk_rows(a->Nout) - 1) / sk_rows(a->Nout));
   const int bm = pick_mtile(a);
   return (int)((Mg + bm - 1) / bm);
@@ -1789,6 +1963,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
   const char* tr = c.transposed ? "true" : "false";
   const char* sc = a->scatter2x2 ? "true" : "false";
   switch (k) {
+    case 'K': snprintf(buf, sizeof buf, "conv3x3_c8_kernel"); break;
     case 'H':
       if (halo8(a))
         snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
@@ -1885,6 +2060,14 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const uint32_t src_bytes = (uint32_t)((uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2);
   const char k = choose(a, dma_fits(a));
+  if (k == 'K') {
+    if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
+    const int TY = (c.Hd + C8_T - 1) / C8_T, TX = (c.Wd + C8_T - 1) / C8_T;
+    const int tiles = c8_tiles(c), grid = c8_grid(a);
+    hipLaunchKernelGGL(conv3x3_c8_kernel, dim3(grid), dim3(256), 0, s, g, TY, TX, tiles / grid, tiles % grid);
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
   if (k == 'H') {
     if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
     int ty, tx;

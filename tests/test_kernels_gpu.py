@@ -179,6 +179,30 @@ def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     assert rel(dx.dense(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,H,W,groups,dcs", [(6, 20, 36, 3, 64), (4, 64, 64, 2, 96), (2, 16, 16, 1, 64)])
+def test_conv3x3_8channel_input(n, H, W, groups, dcs):
+    """The 8-channel-input 3x3 kernel (conv3x3_c8_kernel: halo of 16-B pixel rows, one
+    ds_read_b128 per tap fragment): output (into a wider destination), bias, grouped BN
+    partial statistics against torch fp32 on bf16-rounded operands."""
+    from stfunet import nhwc
+    torch.full((16 << 20,), float("nan"), device=DEV)     # unwritten statistics rows would show as NaN
+    x = bfr(torch.randn(n, 8, H, W, device=DEV))
+    w = bfr(torch.randn(64, 8, 3, 3, device=DEV) / 72 ** 0.5)
+    b = torch.randn(64, device=DEV)
+    ref = F.conv2d(x, w, b, padding=1)
+    wide = nhwc.new_feat(n, H, W, dcs, DEV)
+    dst = wide.slice(0, 64)
+    stats, tiles = nhwc.igemm(feat_from(x), nhwc.pack_weight(w.contiguous(), 0, 8), 64, dst, 3, 3, 1, 1, bias=b,
+                              want_stats=True, groups=groups)
+    out = dst.dense()
+    assert rel(out, ref) < 1e-2
+    st = stats.view(groups, tiles, 2, 64).sum(1)
+    og = out.view(groups, n // groups, 64, H, W)
+    for g in range(groups):
+        assert rel(st[g, 0], og[g].sum((0, 2, 3))) < 2e-3
+        assert rel(st[g, 1], (og[g] ** 2).sum((0, 2, 3))) < 2e-3
+
+
 @pytest.mark.parametrize("n,cin,cout,H,W,R,groups,acc", [
     (16, 512, 512, 8, 8, 3, 8, False),           # STF layer4 shape (per-time-step groups), split 8
     (4, 2048, 1024, 8, 8, 1, 1, False),          # LSTM-backward-like 1x1, split 4
