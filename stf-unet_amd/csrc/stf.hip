@@ -73,6 +73,25 @@ __global__ __launch_bounds__(NT) void stem_im2col_kernel(const float* __restrict
   __syncthreads();
   const int CG = Kpad / 8, Kreal = Cin * KK;
   uint16_t* orow = out + ((long)img * Ho + oy) * Wo * (long)Kpad;
+  if (NT % CG == 0) {
+    // a thread's column group is fixed (NT is a multiple of CG): its 8 (ci, r, s) LDS offsets are
+    // computed once, not per output pixel (the divisions made the kernel VALU-issue bound)
+    const int cg = threadIdx.x % CG;
+    int off[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = cg * 8 + j;
+      const int ci = k / KK, rs = k - ci * KK, r = rs / KS, s = rs - r * KS;
+      off[j] = k < Kreal ? (ci * KS + r) * LW + s : -1;
+    }
+    for (int ox = threadIdx.x / CG; ox < Wo; ox += NT / CG) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = off[j] >= 0 ? rowbuf[off[j] + ox * st] : 0.f;
+      *reinterpret_cast<uint4*>(orow + (long)ox * Kpad + cg * 8) = pack8(v);
+    }
+    return;
+  }
   for (int u = threadIdx.x; u < Wo * CG; u += NT) {
     const int ox = u / CG, cg = u - ox * CG;
     float v[8];
