@@ -26,6 +26,19 @@ STF_DEV void load8f(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// sum over the CG adjacent lanes of a pixel (CG a power of two <= 64), every lane gets it: DPP
+// inside a 16-lane row (quad swaps, half-row and row mirrors -- VALU, no LDS), ds_bpermute
+// (__shfl_xor) only across rows.  (__shfl_xor for every step made head_fwd VALU/LDS-issue bound:
+// 2 TB/s on a 0.29 GB pass.)
+STF_DEV float lane_group_sum(float v, int CG) {
+  if (CG >= 2) v += dpp_f<0xB1>(v);      // quad_perm [1,0,3,2]
+  if (CG >= 4) v += dpp_f<0x4E>(v);      // quad_perm [2,3,0,1]
+  if (CG >= 8) v += dpp_f<0x141>(v);     // row_half_mirror
+  if (CG >= 16) v += dpp_f<0x140>(v);    // row_mirror
+  for (int o = 16; o < CG; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 int head_tiles(long units) {
   long t = (units + NT - 1) / NT;
   return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
@@ -41,9 +54,9 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
   // four 16-B loads are in flight before any arithmetic
   // 32-bit index math (the host checks P * CG < 2^31): 64-bit divisions cost ~40 instructions
   constexpr int U = 4;
-  const int CG = C / 8;
+  const int CG = C / 8, cgs = __builtin_ctz(CG);          // CG is a power of two (head_ok)
   const int units = (int)(P * CG);
-  const int cg = (int)((blockIdx.x * NT + threadIdx.x) % CG);
+  const int cg = (int)((blockIdx.x * NT + threadIdx.x) & (CG - 1));
   float sc[8], sh[8], wk[K][8], bk[K];
   load8f(scale + cg * 8, sc);
   load8f(shift + cg * 8, sh);
@@ -55,7 +68,7 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
 #pragma unroll
     for (int r = 0; r < U; ++r) {
       const int u = u0 + r * stride + threadIdx.x;
-      raw[r] = u < units ? *reinterpret_cast<const uint4*>(y + (size_t)(u / CG) * C + cg * 8) : make_uint4(0, 0, 0, 0);
+      raw[r] = u < units ? *reinterpret_cast<const uint4*>(y + (size_t)(u >> cgs) * C + cg * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int r = 0; r < U; ++r) {
@@ -71,10 +84,9 @@ __global__ void head_fwd_kernel(const uint16_t* __restrict__ y, long P, int HW, 
         for (int k = 0; k < K; ++k) acc[k] += a * wk[k][j];
       }
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        for (int o = 1; o < CG; o <<= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+      for (int k = 0; k < K; ++k) acc[k] = lane_group_sum(acc[k], CG);
       if (u < units && cg == 0) {
-        const int pix = u / CG, n = pix / HW, hw = pix - n * HW;
+        const int pix = u >> cgs, n = pix / HW, hw = pix - n * HW;
 #pragma unroll
         for (int k = 0; k < K; ++k) logits[(size_t)(n * K + k) * HW + hw] = acc[k] + bk[k];
       }
@@ -90,10 +102,10 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_
                                 float* __restrict__ bn_partial, float* __restrict__ head_partial) {
   constexpr int NV = 16 + 8 * K + K;       // sg[8], sgx[8], dW[K][8], db[K]
   __shared__ float red[NT][NV + 1];
-  const int CG = C / 8;
+  const int CG = C / 8, cgs = __builtin_ctz(CG);          // CG is a power of two (head_ok)
   const int units = (int)(P * CG);                // < 2^31 (host check): 32-bit index math
   const int gt = blockIdx.x * NT + threadIdx.x;
-  const int cg = gt % CG;
+  const int cg = gt & (CG - 1);
   float sc[8], sh[8], mu[8], is[8], wk[K][8];
   load8f(scale + cg * 8, sc);
   load8f(shift + cg * 8, sh);
@@ -119,7 +131,7 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, const uint16_
     for (int r = 0; r < U; ++r) {
       const int u = u0 + r * S;
       const bool ok = u < units;
-      const int pix = ok ? u / CG : 0, n = pix / HW, hw = pix - n * HW;
+      const int pix = ok ? u >> cgs : 0, n = pix / HW, hw = pix - n * HW;
       pixr[r] = ok ? pix : -1;
 #pragma unroll
       for (int k = 0; k < K; ++k) dlr[r][k] = ok ? dlogits[(size_t)(n * K + k) * HW + hw] : 0.f;
