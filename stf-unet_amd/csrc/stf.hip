@@ -137,12 +137,12 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
           if (v[j] > mx[j] || am[j] < 0) { mx[j] = v[j]; am[j] = dy * 3 + dx; }
       }
     }
-    *reinterpret_cast<uint4*>(out + p * C + cg * 8) = pack8(mx);
+    *reinterpret_cast<uint4*>(out + (size_t)p * C + cg * 8) = pack8(mx);
     if (argmax) {
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[4 + j] << (8 * j); }
-      *reinterpret_cast<uint2*>(argmax + p * C + cg * 8) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(argmax + (size_t)p * C + cg * 8) = make_uint2(lo, hi);
     }
   }
 }
@@ -155,13 +155,13 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
 __global__ void bn_act_maxpool3_kernel(const uint16_t* __restrict__ y, int N, int H, int W, int C, int Ho, int Wo,
                                        int ipg, const float* __restrict__ scale, const float* __restrict__ shift,
                                        uint16_t* __restrict__ out, uint8_t* __restrict__ argmax) {
-  const int CG = C / 8;
-  const long units = (long)N * Ho * Wo * CG;
-  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
-    const int cg = (int)(u % CG);
-    const long p = u / CG;
-    const int n = (int)(p / ((long)Ho * Wo));
-    const int rem = (int)(p - (long)n * Ho * Wo);
+  // 32-bit index math (the host checks units < 2^31; 64-bit divisions made this VALU-bound)
+  const int CG = C / 8, HoWo = Ho * Wo;
+  const int units = N * HoWo * CG;
+  for (int u = blockIdx.x * NT + threadIdx.x; u < units; u += gridDim.x * NT) {
+    const int p = u / CG, cg = u - p * CG;
+    const int n = p / HoWo;
+    const int rem = p - n * HoWo;
     const int oy = rem / Wo, ox = rem - oy * Wo;
     const int g = n / ipg;
     float sc[8], sh[8];
@@ -357,6 +357,7 @@ extern "C" int stf_bn_act_maxpool3s2(const void* y, int N, int H, int W, int C, 
   if (C % 8 || groups < 1 || N % groups || !y || !scale || !shift || !out) return STF_EINVAL;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long units = (long)N * Ho * Wo * (C / 8);
+  if (units >= (1L << 31) || (long)N * H * W * C >= (1L << 31) * 8L) return STF_EINVAL;
   hipLaunchKernelGGL(bn_act_maxpool3_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
                      (const uint16_t*)y, N, H, W, C, Ho, Wo, N / groups, scale, shift, (uint16_t*)out,
                      (uint8_t*)argmax);
