@@ -46,19 +46,21 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
 
 __global__ void pack_input_kernel(const float* __restrict__ x, int N, int C, int H, int W, int Cpad,
                                   uint16_t* __restrict__ out) {
-  const long HW = (long)H * W, P = N * HW;
+  // 32-bit index math (the host checks N*H*W*Cpad/8 < 2^31): three 64-bit divisions per unit
+  // made this pass VALU-bound (3.3 TB/s on cfg2's 0.2 GB)
+  const int HW = H * W, P = N * HW;
   const int CG = Cpad / 8;
-  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < P * CG; u += (long)gridDim.x * NT) {
-    const long pix = u % P;            // consecutive threads -> consecutive pixels (coalesced reads)
-    const int cg = (int)(u / P);
-    const long n = pix / HW, hw = pix - n * HW;
+  for (int u = blockIdx.x * NT + threadIdx.x; u < P * CG; u += gridDim.x * NT) {
+    const int cg = u / P;
+    const int pix = u - cg * P;        // consecutive threads -> consecutive pixels (coalesced reads)
+    const int n = pix / HW, hw = pix - n * HW;
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = cg * 8 + j;
-      v[j] = c < C ? x[(n * C + c) * HW + hw] : 0.f;
+      v[j] = c < C ? x[((size_t)n * C + c) * HW + hw] : 0.f;
     }
-    *reinterpret_cast<uint4*>(out + pix * Cpad + cg * 8) = pack8(v);
+    *reinterpret_cast<uint4*>(out + (size_t)pix * Cpad + cg * 8) = pack8(v);
   }
 }
 
@@ -298,6 +300,7 @@ extern "C" int stf_adamw(float* p, const float* g, float* m, float* v, int64_t n
 extern "C" int stf_pack_input(const float* x, int N, int C, int H, int W, int Cpad, void* out, stf_stream_t stream) {
   if (Cpad % 8 || Cpad < C) return STF_EINVAL;
   const long units = (long)N * H * W * (Cpad / 8);
+  if (units >= (1L << 31)) return STF_EINVAL;             // 32-bit index math in the kernel
   hipLaunchKernelGGL(pack_input_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream, x, N, C, H,
                      W, Cpad, (uint16_t*)out);
   STF_CHECK_LAUNCH();
