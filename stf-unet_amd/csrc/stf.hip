@@ -120,10 +120,12 @@ __global__ void maxpool3_fwd_kernel(const uint16_t* __restrict__ x, int N, int H
     const int n = (int)(p / ((long)Ho * Wo));
     const int rem = (int)(p - (long)n * Ho * Wo);
     const int oy = rem / Wo, ox = rem - oy * Wo;
+    // every valid tap's value is >= 0 (ReLU) > -inf, so the first valid tap always takes the
+    // maximum and a strict '>' keeps the first maximum in row-major window order
     float mx[8];
     int am[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = -1; }
+    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = 0; }
     for (int dy = 0; dy < 3; ++dy) {
       const int iy = 2 * oy - 1 + dy;
       if (iy < 0 || iy >= H) continue;
@@ -173,10 +175,12 @@ __global__ void bn_act_maxpool3_kernel(const uint16_t* __restrict__ y, int N, in
       sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w; sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
       sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w; sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
     }
+    // every valid tap's value is >= 0 (ReLU) > -inf, so the first valid tap always takes the
+    // maximum and a strict '>' keeps the first maximum in row-major window order
     float mx[8];
     int am[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = -1; }
+    for (int j = 0; j < 8; ++j) { mx[j] = -INFINITY; am[j] = 0; }
     for (int dy = 0; dy < 3; ++dy) {
       const int iy = 2 * oy - 1 + dy;
       if (iy < 0 || iy >= H) continue;
@@ -188,7 +192,7 @@ __global__ void bn_act_maxpool3_kernel(const uint16_t* __restrict__ y, int N, in
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float a = round_e(fmaxf(v[j] * sc[j] + sh[j], 0.f));     // bn_act's stored value
-          if (a > mx[j] || am[j] < 0) { mx[j] = a; am[j] = dy * 3 + dx; }
+          if (a > mx[j]) { mx[j] = a; am[j] = dy * 3 + dx; }
         }
       }
     }
