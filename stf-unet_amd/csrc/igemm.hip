@@ -204,42 +204,60 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
   __syncthreads();
   const int c = tid % CPR, n = n0 + c * 8;
   const bool nok = n < a.Nout;
+  const bool want = a.stats != nullptr;                 // uniform: no unpack / sums without statistics
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  // ConvT 2x2 scatter: the thread's pixel (img, y, x) on the small grid advances RPP rows a
+  // pass, carried instead of divided (the per-pass divisions made the small-K launches
+  // VALU-bound: up128 at 2.9 TB/s)
+  int blk = 0, co = 0, sc_img = 0, sc_y = 0, sc_x = 0;
+  if (SCATTER) {
+    blk = n / Cout; co = n - blk * Cout;
+    const int m = m0 + tid / CPR, hw = a.Hd * a.Wd;
+    sc_img = m / hw;
+    const int rem = m - sc_img * hw;
+    sc_y = rem / a.Wd; sc_x = rem - sc_y * a.Wd;
+  }
 #pragma unroll 4
   for (int ps = 0; ps < PASSES; ++ps) {
     const int row = tid / CPR + ps * RPP;
     const int m = m0 + row;
-    if (!(nok && m < m_end)) continue;
-    uint4 u = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((c ^ (row & 7)) << 4));
-    size_t off;
+    if (nok && m < m_end) {
+      uint4 u = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((c ^ (row & 7)) << 4));
+      size_t off;
+      if (SCATTER) {
+        off = ((size_t)(sc_img * 2 * a.Hd + 2 * sc_y + (blk >> 1)) * (2 * a.Wd) + 2 * sc_x + (blk & 1)) * a.dcs + co;
+      } else if (pcls >= 0) {                        // parity-class row -> output pixel
+        const int py = pcls >> 1, px = pcls & 1;
+        const int Hc = (a.Hd - py + 1) >> 1, Wc = (a.Wd - px + 1) >> 1;
+        const int img = m / (Hc * Wc), rem = m - img * (Hc * Wc), uu = rem / Wc, v = rem - uu * Wc;
+        off = ((size_t)(img * a.Hd + 2 * uu + py) * a.Wd + 2 * v + px) * a.dcs + n;
+      } else {
+        off = (size_t)m * a.dcs + n;
+      }
+      if (a.accumulate || want) {
+        float f[8];
+        unpack8(u, f);
+        if (a.accumulate) {
+          float o[8];
+          unpack8(*reinterpret_cast<const uint4*>(a.dst + off), o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = round_e(f[e] + o[e]);
+          u = pack8(f);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
+      }
+      *reinterpret_cast<uint4*>(a.dst + off) = u;
+    }
     if (SCATTER) {
-      const int blk = n / Cout, co = n - blk * Cout;
-      const int hw = a.Hd * a.Wd;
-      const int img = m / hw, rem = m - img * hw;
-      const int yd = rem / a.Wd, xd = rem - yd * a.Wd;
-      off = ((size_t)(img * 2 * a.Hd + 2 * yd + (blk >> 1)) * (2 * a.Wd) + 2 * xd + (blk & 1)) * a.dcs + co;
-    } else if (pcls >= 0) {                          // parity-class row -> output pixel
-      const int py = pcls >> 1, px = pcls & 1;
-      const int Hc = (a.Hd - py + 1) >> 1, Wc = (a.Wd - px + 1) >> 1;
-      const int img = m / (Hc * Wc), rem = m - img * (Hc * Wc), u = rem / Wc, v = rem - u * Wc;
-      off = ((size_t)(img * a.Hd + 2 * u + py) * a.Wd + 2 * v + px) * a.dcs + n;
-    } else {
-      off = (size_t)m * a.dcs + n;
+      sc_x += RPP;
+      while (sc_x >= a.Wd) {
+        sc_x -= a.Wd;
+        if (++sc_y == a.Hd) { sc_y = 0; ++sc_img; }
+      }
     }
-    float f[8];
-    unpack8(u, f);
-    if (a.accumulate) {
-      float o[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.dst + off), o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = round_e(f[e] + o[e]);
-      u = pack8(f);
-    }
-    *reinterpret_cast<uint4*>(a.dst + off) = u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] += f[e]; s2[e] += f[e] * f[e]; }
   }
   if (a.stats == nullptr) return;
   // threads with equal c: fold within the wave (lanes c, c+CPR, ...), then over waves
@@ -603,7 +621,8 @@ STF_DEV int swzk(int row, int kc) {
 // every lane gathers its own tap (k-step = 4 taps at BKK 32); K need not be a
 // multiple of BKK (k >= K masked)
 template <int BM, int BN, int WM, int WN, int BKK, int STAGES, bool TRANS, bool SCATTER, int EPI, bool C8 = false>
-__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4) ? 2 : 1) void igemm_dma_kernel(Geo a, uint32_t src_bytes) {
+__global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 || (BM == 128 && BN == 256)) ? 2 : 1) void igemm_dma_kernel(
+    Geo a, uint32_t src_bytes) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1714,11 +1733,12 @@ constexpr Cfg CFG_B{256, 128, 64};   // 8 waves (4x2), 3 stages
 constexpr Cfg CFG_C{256, 256, 64};   // 8 waves (2x4), 2 stages
 constexpr Cfg CFG_D{512, 64, 64};    // 8 waves (8x1), 2 stages
 constexpr Cfg CFG_E{256, 64, 32};    // 4 waves (4x1), 4 stages, 2 blocks/CU
+constexpr Cfg CFG_F{128, 256, 32};   // 8 waves (2x4), 2 stages, 2 blocks/CU (80 KiB each)
 
 char forced_cfg() {
   static const char c = [] {
     const char* e = getenv("STF_IGEMM_CFG");
-    return (e && ((e[0] >= 'A' && e[0] <= 'E') || e[0] == 'H' || e[0] == 'L')) ? e[0] : '0';
+    return (e && ((e[0] >= 'A' && e[0] <= 'F') || e[0] == 'H' || e[0] == 'L')) ? e[0] : '0';
   }();
   return c;
 }
@@ -1795,6 +1815,7 @@ Cfg cfg_of(char k) {
     case 'C': return CFG_C;
     case 'D': return CFG_D;
     case 'E': return CFG_E;
+    case 'F': return CFG_F;
     default: return CFG_A;
   }
 }
@@ -1909,7 +1930,7 @@ int ksplit_of(const stf_igemm_args* a) {
   const stf_conv_geom& c = a->g;
   const char k = choose(a, dma_fits(a));
   if (!on || a->lstm || a->scatter2x2 || c.transposed || c.Cs == 8) return 1;
-  if (!(k == 'A' || k == 'B' || k == 'C' || k == 'D' || k == 'E')) return 1;
+  if (!(k == 'A' || k == 'B' || k == 'C' || k == 'D' || k == 'E' || k == 'F')) return 1;
   if (a->Nout % 8 || NT % (a->Nout / 8) || a->dst_cstride % 8 || ((uintptr_t)a->dst & 15)) return 1;
   const Cfg f = cfg_of(k);
   const long M = (long)c.N * c.Hd * c.Wd;
@@ -1982,6 +2003,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
     case 'B': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 128, 4, 2, 64, 3, false, %s, %d, false>", sc, epi); break;
     case 'C': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 256, 2, 4, 64, 2, false, %s, %d, false>", sc, epi); break;
     case 'D': snprintf(buf, sizeof buf, "igemm_dma_kernel<512, 64, 8, 1, 64, 2, false, %s, %d, false>", sc, epi); break;
+    case 'F': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 256, 2, 4, 32, 2, false, %s, 0, false>", sc); break;
     default: {
       const bool small = (a->Nout <= 64 && !a->lstm);
       snprintf(buf, sizeof buf, "igemm_kernel<%s, %s, %s, %s, %d>", small ? "256, 64, 4, 1" : "128, 128, 2, 2",
@@ -2147,6 +2169,15 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     case 'B': launch_dma_plain<256, 128, 4, 2, 64, 3>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
     case 'C': launch_dma_plain<256, 256, 2, 4, 64, 2>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
     case 'D': launch_dma_plain<512, 64, 8, 1, 64, 2>(g, a->scatter2x2, src_bytes, s, lstm_epi); break;
+    case 'F': {                                    // plain gathers and the ConvT scatter only
+      if (lstm_epi) return STF_EINVAL;
+      dim3 grid(g.tpg * ((g.M + g.Mg - 1) / g.Mg), (g.Nout + 255) / 256, g.ksplit), block(512);
+      if (a->scatter2x2)
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 256, 2, 4, 32, 2, false, true, 0>), grid, block, 0, s, g, src_bytes);
+      else
+        hipLaunchKernelGGL((igemm_dma_kernel<128, 256, 2, 4, 32, 2, false, false, 0>), grid, block, 0, s, g, src_bytes);
+      break;
+    }
     default:
       if (bm == 256) return launch_reg<256, 64, 4, 1>(g, smallc, c.transposed, a->scatter2x2, lstm_epi, s);
       return launch_reg<128, 128, 2, 2>(g, smallc, c.transposed, a->scatter2x2, lstm_epi, s);
