@@ -208,16 +208,17 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  // ConvT 2x2 scatter: the thread's pixel (img, y, x) on the small grid advances RPP rows a
-  // pass, carried instead of divided (the per-pass divisions made the small-K launches
-  // VALU-bound: up128 at 2.9 TB/s)
-  int blk = 0, co = 0, sc_img = 0, sc_y = 0, sc_x = 0;
+  // ConvT 2x2 scatter: the thread's pixel advances RPP rows a pass; its column x on the small
+  // grid and its output offset are carried with adds (+2 dcs per pixel, +2 Wd dcs more per
+  // small-grid row; image rows follow each other, so an image boundary needs nothing extra)
+  // instead of per-pass divisions, which made the small-K launches VALU-bound (up128 2.9 TB/s)
+  int sc_x = 0;
+  size_t sc_off = 0;
   if (SCATTER) {
-    blk = n / Cout; co = n - blk * Cout;
-    const int m = m0 + tid / CPR, hw = a.Hd * a.Wd;
-    sc_img = m / hw;
-    const int rem = m - sc_img * hw;
-    sc_y = rem / a.Wd; sc_x = rem - sc_y * a.Wd;
+    const int blk = n / Cout, co = n - blk * Cout;
+    const int m = m0 + tid / CPR, gy = m / a.Wd;      // global small-grid row (img * Hd + y)
+    sc_x = m - gy * a.Wd;
+    sc_off = ((size_t)(2 * gy + (blk >> 1)) * (2 * a.Wd) + 2 * sc_x + (blk & 1)) * a.dcs + co;
   }
 #pragma unroll 4
   for (int ps = 0; ps < PASSES; ++ps) {
@@ -227,7 +228,7 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
       uint4 u = *reinterpret_cast<const uint4*>(smem + row * (BN * 2) + ((c ^ (row & 7)) << 4));
       size_t off;
       if (SCATTER) {
-        off = ((size_t)(sc_img * 2 * a.Hd + 2 * sc_y + (blk >> 1)) * (2 * a.Wd) + 2 * sc_x + (blk & 1)) * a.dcs + co;
+        off = sc_off;
       } else if (pcls >= 0) {                        // parity-class row -> output pixel
         const int py = pcls >> 1, px = pcls & 1;
         const int Hc = (a.Hd - py + 1) >> 1, Wc = (a.Wd - px + 1) >> 1;
@@ -253,9 +254,10 @@ STF_DEV void staged_epilogue(const Geo& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 
     }
     if (SCATTER) {
       sc_x += RPP;
+      sc_off += (size_t)(2 * RPP) * a.dcs;
       while (sc_x >= a.Wd) {
         sc_x -= a.Wd;
-        if (++sc_y == a.Hd) { sc_y = 0; ++sc_img; }
+        sc_off += (size_t)(2 * a.Wd) * a.dcs;
       }
     }
   }
