@@ -469,17 +469,20 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_dma_kernel(WArgs a, int tiles_
 // kernel reads dy four times) and each tap's transposed reads hit consecutive
 // rows.  Single LDS buffer (51 KB) -> 3 blocks per CU; the next tile's global
 // loads are in flight (registers) during the MFMAs of the current one.
-template <int PW>
-__global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles) {
+// NB = 2: a block covers 128 dy channels (two 64-channel LDS sub-tiles, 61 KB, 2 blocks
+// per CU), so the 2x larger x tensor crosses HBM once per 128 dy channels, not per 64.
+template <int PW, int NB>
+__global__ __launch_bounds__(NT, NB == 1 ? 3 : 2) void wgrad2x2s2_kernel(WArgs a, int tiles_y, int tiles_x,
+                                                                          int ntiles) {
   constexpr int PH = 64 / PW, SR = 64 + 16;
-  constexpr int A_EL = 64 * SR, B_EL = 4 * 64 * SR;
-  constexpr int CHA = 64 * 8 / NT, CHB = 4 * 64 * 8 / NT;
+  constexpr int A_EL = NB * 64 * SR, B_EL = 4 * 64 * SR;
+  constexpr int CHA = NB * 64 * 8 / NT, CHB = 4 * 64 * 8 / NT;
   __shared__ __attribute__((aligned(16))) uint16_t smem[A_EL + B_EL];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int TMW = 4;                        // all 64 dy channels per wave, 16 x channels (wave)
+  constexpr int TMW = 4 * NB;                   // all 64 NB dy channels per wave, 16 x channels (wave)
   const int split = blockIdx.x;
-  const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
+  const int n0 = blockIdx.y * 64 * NB, c0 = blockIdx.z * 64;
   const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
   const int per_img = tiles_y * tiles_x;
 
@@ -490,11 +493,12 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
     const int y0 = ty * PH, x0 = tx * PW;
 #pragma unroll
     for (int i = 0; i < CHA; ++i) {
-      const int e = tid + i * NT, px = e >> 3, ch = e & 7;
+      const int e = tid + i * NT, sub = e >> 9, px = (e >> 3) & 63, ch = e & 7;   // sub-tile, pixel, chunk
       const int yd = y0 + px / PW, xd = x0 + px % PW;
       ra[i] = make_uint4(0, 0, 0, 0);
       if (yd < a.Hd && xd < a.Wd)
-        ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
+        ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 +
+                                                sub * 64 + ch * 8);
     }
 #pragma unroll
     for (int i = 0; i < CHB; ++i) {
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
     uint16_t* sb = smem + A_EL;
 #pragma unroll
     for (int i = 0; i < CHA; ++i) {
-      const int e = tid + i * NT;
+      const int e = tid + i * NT;                   // sub-tile e >> 9 starts at row 64 (e >> 9)
       *reinterpret_cast<uint4*>(sa + (e >> 3) * SR + (e & 7) * 8) = ra[i];
     }
 #pragma unroll
@@ -549,7 +553,7 @@ __global__ __launch_bounds__(NT, 3) void wgrad2x2s2_kernel(WArgs a, int tiles_y,
       e16x8 af[TMW];
 #pragma unroll
       for (int i = 0; i < TMW; ++i) {
-        const int col = i * 16 + p4;
+        const int col = (i >> 2) * 64 * SR + (i & 3) * 16 + p4;
         v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][0] + col));
         v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(sa + prow[k2][1] + col));
         short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -703,6 +707,15 @@ int fused22_pw(const stf_wgrad_args* a) {
   return c.Wd >= 16 ? 16 : 8;
 }
 
+// dy channels per ConvT 2x2 block, in 64s: 2 from 256 dy channels up (measured, tools/ab_convt.sh,
+// batch 64: up16/32/64 132/127/134 -> 104/99/107 us; at 128 channels the two 64-channel blocks
+// of a pixel tile meet in L2 anyway and the 3-per-CU occupancy wins, 150 vs 172 us).
+// STF_WGRAD22_NB=1: always 1 (A/B)
+int fused22_nb(const stf_wgrad_args* a) {
+  static const int force1 = [] { const char* e = getenv("STF_WGRAD22_NB"); return e && e[0] == '1'; }();
+  return (!force1 && a->Nout % 128 == 0 && a->Nout >= 256) ? 2 : 1;
+}
+
 void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
   ty = (a->g.Hd + 64 / pw - 1) / (64 / pw);
   tx = (a->g.Wd + pw - 1) / pw;
@@ -713,7 +726,7 @@ void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
   if (const int pw = fused_pw(a) ? fused_pw(a) : fused22_pw(a)) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
-    const long tiles = (long)(a->Nout / 64) * (a->g.Cs / 64);
+    const long tiles = (long)(a->Nout / (fused_pw(a) ? 64 : 64 * fused22_nb(a))) * (a->g.Cs / 64);
     const long target = a->grid_blocks > 0 ? a->grid_blocks : 512;
     long want = (target + tiles - 1) / tiles;
     const long maxs = (nt + 3) / 4;                  // at least 4 pixel tiles per split
@@ -751,7 +764,10 @@ extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
     if (wgrad_dma(a)) return pw == 16 ? "wgrad3x3_dma_kernel<16>" : "wgrad3x3_dma_kernel<8>";
     return pw == 16 ? "wgrad3x3_kernel<16, 0>" : "wgrad3x3_kernel<8, 0>";
   }
-  if (const int pw = fused22_pw(a)) return pw == 16 ? "wgrad2x2s2_kernel<16>" : "wgrad2x2s2_kernel<8>";
+  if (const int pw = fused22_pw(a)) {
+    if (fused22_nb(a) == 2) return pw == 16 ? "wgrad2x2s2_kernel<16, 2>" : "wgrad2x2s2_kernel<8, 2>";
+    return pw == 16 ? "wgrad2x2s2_kernel<16, 1>" : "wgrad2x2s2_kernel<8, 1>";
+  }
   if (big_tile(a)) return "wgrad_kernel<128, 128, 32, false>";
   const int rsc = a->g.R * a->g.S * a->g.Cs;
   if (a->g.Cs % 64 == 0) return "wgrad_kernel<64, 64, 64, false>";
@@ -799,11 +815,12 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   } else if (const int pw22 = fused22_pw(a)) {
     int ty, tx, nt;
     fused_tiles(a, pw22, ty, tx, nt);
-    dim3 grid(splits, a->Nout / 64, c.Cs / 64);
-    if (pw22 == 16)
-      hipLaunchKernelGGL((wgrad2x2s2_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
-    else
-      hipLaunchKernelGGL((wgrad2x2s2_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    const int nb = fused22_nb(a);
+    dim3 grid(splits, a->Nout / (64 * nb), c.Cs / 64);
+    if (nb == 2 && pw22 == 16) hipLaunchKernelGGL((wgrad2x2s2_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (nb == 2) hipLaunchKernelGGL((wgrad2x2s2_kernel<8, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (pw22 == 16) hipLaunchKernelGGL((wgrad2x2s2_kernel<16, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else hipLaunchKernelGGL((wgrad2x2s2_kernel<8, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
   } else if (big_tile(a)) {
     dim3 grid(splits, a->Nout / 128, rsc / 128);
     hipLaunchKernelGGL((wgrad_kernel<128, 128, 32, false>), grid, dim3(NT), 0, s, w);

@@ -297,7 +297,7 @@ def test_conv_into_concat_slice():
     assert full[:, :64].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("cin,cout,h", [(128, 64, 8), (1024, 512, 4), (64, 32, 16)])
+@pytest.mark.parametrize("cin,cout,h", [(128, 64, 8), (1024, 512, 4), (64, 32, 16), (256, 128, 8)])
 def test_convT2x2_fwd_dgrad_wgrad(cin, cout, h):
     from stfunet import nhwc
     x = bfr(torch.randn(2, cin, h, h, device=DEV))

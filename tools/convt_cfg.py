@@ -25,7 +25,7 @@ def timeit(fn):
 
 
 cfg = os.environ.get("STF_IGEMM_CFG", "auto")
-tf_tot = td_tot = 0.0
+tf_tot = td_tot = tw_tot = 0.0
 for h, cin in ((16, 1024), (32, 512), (64, 256), (128, 128)):
     cout = cin // 2
     x = nhwc.new_feat(B, h, h, cin, "cuda")
@@ -44,9 +44,12 @@ for h, cin in ((16, 1024), (32, 512), (64, 256), (128, 128)):
     dy = nhwc.new_feat(B, 2 * h, 2 * h, cout, "cuda")
     dy.buf.normal_()
     td = timeit(lambda: nhwc.igemm(dy, w3, cin, x, 2, 2, 2, 0))
+    dw = torch.empty(cin * cout * 4, device="cuda")
+    tw = timeit(lambda: nhwc.wgrad(x, dy, 2, 2, 2, 0, dw))
     mb = (B * h * h * cin * 2 + 4 * B * h * h * cout * 2) / 1e6
     print(f"cfg {cfg}  up{h:<4d} {cin:5d}->{cout:5d}  fwd {tf:7.1f} us ({mb / tf:5.2f} TB/s alg; dense dst {tfd:6.1f} us, its zero_ {tz:6.1f} us)  "
-          f"dgrad {td:7.1f} us", flush=True)
+          f"dgrad {td:7.1f} us  wgrad {tw:7.1f} us", flush=True)
     tf_tot += tf
     td_tot += td
-print(f"cfg {cfg}  TOTAL fwd {tf_tot:.1f} us  dgrad {td_tot:.1f} us", flush=True)
+    tw_tot += tw
+print(f"cfg {cfg}  TOTAL fwd {tf_tot:.1f} us  dgrad {td_tot:.1f} us  wgrad {tw_tot:.1f} us", flush=True)
