@@ -412,7 +412,7 @@ class STFProgram:
         B, Ttot, Cf, H, W = x.shape
         P = m.pk_channels if m.use_pk_maps else 0
         T = Ttot - P
-        assert T >= 1 and H % 32 == 0 and W % 32 == 0, "STFLSTMUNet needs H, W divisible by 32"
+        _check_input_shape(x.shape, P)
         x = x.contiguous().float()
         S = _S()
         S.B, S.T, S.P, S.H, S.W = B, T, P, H, W
@@ -651,6 +651,22 @@ class STFProgram:
         return dpk.slice(0, C)
 
 
+def _check_input_shape(shape, P):
+    """[B, T + P, C, H, W] with at least one frame, H and W divisible by 32.
+
+    For other sizes the reference's decoder resizes the transposed-conv output to the skip
+    size by bilinear interpolation (src/stf_lstm_unet.py:56-57); that edge path is not
+    implemented here and is refused up front rather than mis-tiled."""
+    if len(shape) != 5:
+        raise ValueError(f"STFLSTMUNet expects [B, T, C, H, W], got shape {tuple(shape)}")
+    Ttot, H, W = shape[1], shape[3], shape[4]
+    if Ttot - P < 1:
+        raise ValueError(f"STFLSTMUNet: {Ttot} input frames leave no time steps after {P} PK maps")
+    if H % 32 or W % 32:
+        raise ValueError(f"STFLSTMUNet needs H, W divisible by 32 (got {H}x{W}); the reference's "
+                         "bilinear size fallback (src/stf_lstm_unet.py:56-57) is not supported")
+
+
 class _STFFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, prog, storage, *params):
@@ -720,6 +736,7 @@ class STFLSTMUNet(nn.Module):
 
     def forward(self, x, pk_maps=None):
         # pk_maps is ignored, as in the reference (PK maps ride on the T axis, :146-156)
+        _check_input_shape(x.shape, self.pk_channels if self.use_pk_maps else 0)
         if not x.is_cuda:
             raise RuntimeError("stfunet.STFLSTMUNet runs on the gfx950 HIP kernels only; move the model and "
                                "input to a ROCm device (no CPU fallback)")

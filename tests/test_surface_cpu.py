@@ -236,6 +236,23 @@ def test_stf_accepts_reference_state_dict_roundtrip():
     assert torch.equal(m.state_dict()["lstm4.weight_hh_l0"], torch.full((2048, 512), 0.5))
 
 
+def test_stf_refuses_unsupported_shapes_up_front():
+    """H, W not divisible by 32 take the reference's bilinear size fallback
+    (src/stf_lstm_unet.py:56-57), which is not implemented: refused with a ValueError naming
+    it before any device work; too few frames for the PK maps likewise."""
+    from stfunet import STFLSTMUNet
+    m = STFLSTMUNet(time_steps=4)
+    with pytest.raises(ValueError, match="divisible by 32.*bilinear size fallback"):
+        m(torch.zeros(1, 4, 1, 48, 64))
+    with pytest.raises(ValueError, match=r"\[B, T, C, H, W\]"):
+        m(torch.zeros(4, 1, 64, 64))
+    mp = STFLSTMUNet(time_steps=4, use_pk_maps=True)
+    with pytest.raises(ValueError, match="no time steps"):
+        mp(torch.zeros(1, mp.pk_channels, 1, 64, 64))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):     # valid shape: the device guard
+        m(torch.zeros(1, 4, 1, 64, 64))
+
+
 def test_epoch_results_file_and_checkpoint_dict(tmp_path):
     """train.py:151-162 results-file name, the per-epoch block of :289-301, the checkpoint
     dict of :304-311 (+ 'scaler' under --amp), resume_from (:249-256) and EarlyStopping
