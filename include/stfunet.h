@@ -394,12 +394,15 @@ int stf_lstm_seq_bwd(const void* wcat, const void* wcat_t, const float* bias, co
  * the launch (agent-scope counters, write-through stores, an acquire per step).  Same
  * arguments, layout and values (bit for bit) as stf_lstm_seq_fwd / the per-step path, plus
  * `sync`: a caller-owned device buffer of stf_lstm_coop_sync_bytes(P, T) bytes (16-B aligned;
- * zeroed on the stream by the call itself; its last word is an error flag that
- * stf_lstm_coop_error copies out: nonzero = a step's hand-off timed out).  ABI v9. */
+ * zeroed on the stream by the call itself; its last word is an error flag: nonzero = a step's
+ * hand-off timed out, after which the launch drains at once with wrong values).  spin_limit: polls
+ * before a hand-off gives up (0 = the default, ~4 s; 0xFFFFFFFF = every hand-off reports a timeout
+ * at once: the error path, for tests).  ABI v12. */
 size_t stf_lstm_coop_sync_bytes(int P, int T);
 int stf_lstm_coop_supported(int C);
 int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
-                      void* h_last, int h_cstride, float* gates, unsigned* sync, int max_wg, stf_stream_t stream);
+                      void* h_last, int h_cstride, float* gates, unsigned* sync, int max_wg, unsigned spin_limit,
+                      stf_stream_t stream);
 /* gates (or NULL): [T][P][4C] fp32 activated gates (i, f, g, o interleaved per channel), kept
  * for stf_lstm_coop_bwd: the BPTT of the same sequence in one persistent launch (same
  * workgroup grid; per step the C/32 workgroups of a pixel block exchange the dgates rows and
@@ -411,8 +414,19 @@ int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, in
  * other work leaves the rest of the chip to it (a group of C/32 must fit). */
 int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, int C,
                       const void* dh_last, int dh_cstride, void* dgates, void* dx, int dx_cstride,
-                      unsigned* sync, int max_wg, stf_stream_t stream);
-int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* out, stf_stream_t stream);
+                      unsigned* sync, int max_wg, unsigned spin_limit, stf_stream_t stream);
+/* sticky |= the error word of the launch that used `sync` (stream-ordered, no host sync): a program
+ * keeps one sticky device word across steps and reads it back at a step boundary. */
+int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* sticky, stf_stream_t stream);
+/* The DecoderBlock's size fallback (src/stf_lstm_unet.py:56-57): F.interpolate(mode="bilinear",
+ * align_corners=True) of x [N][H][W] (C channels, stride x_cstride, 16-bit NHWC) to y [N][h][w]
+ * (stride y_cstride; e.g. the concat slice), PyTorch's coordinate arithmetic; and its backward,
+ * dx [N][H][W] = the gather of dy [N][h][w] (no atomics: each input pixel sums the output pixels
+ * that read it, in a fixed order).  C % 8 == 0, strides % 8 == 0, 16-B aligned.  ABI v12. */
+int stf_bilinear_ac_fwd(const void* x, int N, int H, int W, int C, int x_cstride, void* y, int h, int w,
+                        int y_cstride, stf_stream_t stream);
+int stf_bilinear_ac_bwd(const void* dy, int N, int h, int w, int C, int dy_cstride, void* dx, int H, int W,
+                        int dx_cstride, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
 int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,
                          float* dw_hh, float* db_ih, float* db_hh, stf_stream_t stream);

@@ -202,6 +202,10 @@ inline void launch(void (*k)(A...), dim3 g, dim3 b, unsigned sh, hipStream_t s, 
 }
 
 hipError_t memset_async(void* p, int value, size_t bytes, hipStream_t s);
+// Timing-only ablation knobs (results are WRONG while one is on: STF_HALO_DIAG, STF_WGRAD_DIAG,
+// STF_WGRAD_ONE_SLAB) take effect only with STF_ABLATION=1 also set; otherwise a set knob is
+// refused with one line on stderr and reads as 0.  Defined in plan.hip.
+int ablation_env(const char* name);
 hipError_t memcpy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
 }  // namespace stf
 

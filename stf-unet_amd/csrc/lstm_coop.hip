@@ -37,7 +37,25 @@
 namespace {
 
 constexpr int CNT = 256, CBM = 64, CR = 128;      // threads, pixels per block, gate rows per slice
-constexpr unsigned SPIN_LIMIT = 1u << 25;          // ~4 s of s_sleep(2) polls
+constexpr unsigned SPIN_LIMIT = 1u << 25;          // ~4 s of s_sleep(2) polls (spin_limit = 0)
+
+// consumer side of a hand-off (one lane): poll counter c until it reads S.  A poll count past
+// `limit` sets the launch's error word and gives up; once the word is set anywhere in the
+// launch every later wait gives up at once (a stalled launch drains in one timeout, not one
+// per step and block).  The caller turns the word into a Python RuntimeError
+// (stf_lstm_coop_error -> STFProgram.check_device_errors).
+STF_DEV void coop_wait(unsigned* c, unsigned S, unsigned* err, unsigned limit) {
+  if (limit == 0xFFFFFFFFu) {            // STF_COOP_FORCE_TIMEOUT: every hand-off "times out" (tests)
+    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  unsigned spins = 0;
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+    if ((spins & 255u) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > limit) { __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+  }
+}
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -49,7 +67,8 @@ template <int C>
 __global__ __launch_bounds__(CNT, 1) void lstm_coop_fwd_kernel(const uint16_t* __restrict__ wcat,
                                                                const float* __restrict__ bias, uint16_t* lbuf, int P,
                                                                int T, float* __restrict__ cst, uint16_t* hT, int hTcs,
-                                                               float* __restrict__ gates, unsigned* cnt, unsigned* err) {
+                                                               float* __restrict__ gates, unsigned* cnt, unsigned* err,
+                                                               unsigned limit) {
   constexpr int S = 4 * C / CR;            // slices (workgroups per pixel block)
   constexpr int KS = 2 * C / 32;           // k-steps: x (KS/2) then h (KS/2)
   constexpr int NF = 2;                    // 32 gate rows per wave
@@ -127,11 +146,7 @@ __global__ __launch_bounds__(CNT, 1) void lstm_coop_fwd_kernel(const uint16_t* _
       if (t > 0) {
         // wait for the S slices of h_{t-1}, one agent-scope acquire, then its rows
         if (tid == 0) {
-          unsigned spins = 0;
-          while (__hip_atomic_load(&cnt[pb * T + t - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > SPIN_LIMIT) { __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-          }
+          coop_wait(&cnt[pb * T + t - 1], (unsigned)S, err, limit);
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -209,7 +224,7 @@ __global__ __launch_bounds__(CNT, 1) void lstm_coop_bwd_kernel(const uint16_t* _
                                                                const float* __restrict__ cst, int P, int T,
                                                                const uint16_t* __restrict__ dhT, int dhcs,
                                                                uint16_t* dg, uint16_t* d2, int d2cs, unsigned* cnt,
-                                                               unsigned* err) {
+                                                               unsigned* err, unsigned limit) {
   constexpr int S = 4 * C / CR;
   constexpr int K2 = 4 * C / 32;           // k-steps of the dgates x W GEMM
   constexpr int NF = 2, MF = CBM / 16;
@@ -241,11 +256,7 @@ __global__ __launch_bounds__(CNT, 1) void lstm_coop_bwd_kernel(const uint16_t* _
 
   auto wait_for = [&](unsigned* c) {
     if (tid == 0) {
-      unsigned spins = 0;
-      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)S) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > SPIN_LIMIT) { __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-      }
+      coop_wait(c, (unsigned)S, err, limit);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -393,7 +404,7 @@ int grid_of(int P, int max_wg) {
 
 template <int C>
 int launch_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, float* c_out, void* h_last,
-               int h_cstride, float* gates, unsigned* sync, int max_wg, hipStream_t s) {
+               int h_cstride, float* gates, unsigned* sync, int max_wg, unsigned limit, hipStream_t s) {
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;      // counters + the error word
@@ -401,14 +412,15 @@ int launch_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, fl
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_coop_fwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat, bias,
                      (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride, gates, sync,
-                     sync + 2 * (size_t)npb * T);
+                     sync + 2 * (size_t)npb * T, limit);
   STF_CHECK_LAUNCH();
   return 0;
 }
 
 template <int C>
 int launch_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, const void* dh_last,
-               int dh_cstride, void* dgates, void* dx, int dx_cstride, unsigned* sync, int max_wg, hipStream_t s) {
+               int dh_cstride, void* dgates, void* dx, int dx_cstride, unsigned* sync, int max_wg, unsigned limit,
+               hipStream_t s) {
   if (num_cus() <= 0) return STF_EINVAL;
   const int npb = (P + CBM - 1) / CBM;
   const size_t words = 2 * (size_t)npb * T + 1;
@@ -416,7 +428,7 @@ int launch_bwd(const void* wcat_t, const float* gates, const float* c_all, int P
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL((lstm_coop_bwd_kernel<C>), dim3(grid_of<C>(P, max_wg)), dim3(CNT), 0, s, (const uint16_t*)wcat_t, gates,
                      c_all, P, T, (const uint16_t*)dh_last, dh_cstride, (uint16_t*)dgates, (uint16_t*)dx, dx_cstride,
-                     sync, sync + 2 * (size_t)npb * T);
+                     sync, sync + 2 * (size_t)npb * T, limit);
   STF_CHECK_LAUNCH();
   return 0;
 }
@@ -432,7 +444,7 @@ extern "C" int stf_lstm_coop_supported(int C) { return C == 128 || C == 256 || C
 
 extern "C" int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf, int P, int T, int C, float* c_out,
                                  void* h_last, int h_cstride, float* gates, unsigned* sync, int max_wg,
-                                 stf_stream_t stream) {
+                                 unsigned spin_limit, stf_stream_t stream) {
   if (P <= 0 || T <= 0) return 0;
   if (!stf_lstm_coop_supported(C) || !wcat || !bias || !lbuf || !c_out || !h_last || !sync || h_cstride < C ||
       h_cstride % 8)
@@ -442,16 +454,17 @@ extern "C" int stf_lstm_coop_fwd(const void* wcat, const float* bias, void* lbuf
     return STF_EINVAL;
   if ((size_t)T * P * 2 * C * 2 >= 0xFFFFFF00ull) return STF_EINVAL;     // 32-bit buffer offsets
   hipStream_t s = (hipStream_t)stream;
+  const unsigned lim = spin_limit ? spin_limit : SPIN_LIMIT;
   switch (C) {
-    case 128: return launch_fwd<128>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
-    case 256: return launch_fwd<256>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
-    default: return launch_fwd<512>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, s);
+    case 128: return launch_fwd<128>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, lim, s);
+    case 256: return launch_fwd<256>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, lim, s);
+    default: return launch_fwd<512>(wcat, bias, lbuf, P, T, c_out, h_last, h_cstride, gates, sync, max_wg, lim, s);
   }
 }
 
 extern "C" int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const float* c_all, int P, int T, int C,
                                  const void* dh_last, int dh_cstride, void* dgates, void* dx, int dx_cstride,
-                                 unsigned* sync, int max_wg, stf_stream_t stream) {
+                                 unsigned* sync, int max_wg, unsigned spin_limit, stf_stream_t stream) {
   if (P <= 0 || T <= 0) return 0;
   if (!stf_lstm_coop_supported(C) || !wcat_t || !gates || !c_all || !dh_last || !dgates || !dx || !sync ||
       dh_cstride < C || dx_cstride < 2 * C || dx_cstride % 8)
@@ -462,14 +475,26 @@ extern "C" int stf_lstm_coop_bwd(const void* wcat_t, const float* gates, const f
   if ((size_t)T * P * 4 * C * 2 >= 0xFFFFFF00ull || (size_t)T * P * dx_cstride * 2 >= 0xFFFFFF00ull)
     return STF_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  const unsigned lim = spin_limit ? spin_limit : SPIN_LIMIT;
   switch (C) {
-    case 128: return launch_bwd<128>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
-    case 256: return launch_bwd<256>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
-    default: return launch_bwd<512>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, s);
+    case 128: return launch_bwd<128>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, lim, s);
+    case 256: return launch_bwd<256>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, lim, s);
+    default: return launch_bwd<512>(wcat_t, gates, c_all, P, T, dh_last, dh_cstride, dgates, dx, dx_cstride, sync, max_wg, lim, s);
   }
 }
 
-extern "C" int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* out, stf_stream_t stream) {
+namespace {
+__global__ void coop_error_or_kernel(const unsigned* __restrict__ word, unsigned* __restrict__ sticky) {
+  if (threadIdx.x == 0 && *word) *sticky |= 1u;
+}
+}  // namespace
+
+// sticky |= (the launch's error word), stream-ordered: a caller keeps one sticky word per program
+// across steps and reads it back at a step boundary (no host sync on the step's path)
+extern "C" int stf_lstm_coop_error(const unsigned* sync, int P, int T, unsigned* sticky, stf_stream_t stream) {
+  if (!sync || !sticky || P <= 0 || T <= 0) return STF_EINVAL;
   const size_t npb = (size_t)(P + CBM - 1) / CBM;
-  return (int)stf::memcpy_async(out, sync + 2 * npb * T, 4, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  hipLaunchKernelGGL(coop_error_or_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, sync + 2 * npb * T, sticky);
+  STF_CHECK_LAUNCH();
+  return 0;
 }

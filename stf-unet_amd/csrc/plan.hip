@@ -19,6 +19,8 @@
 #include "../../include/stfunet.h"
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -141,6 +143,18 @@ __global__ void i64_add_kernel(I64Batch b, int n, int64_t inc) {
 bool stf::plan_recording() { return g_rec != nullptr; }
 
 void stf::plan_append(stf::PlanOp* op, hipStream_t s) { append(op, s); }
+
+int stf::ablation_env(const char* name) {
+  const char* e = getenv(name);
+  if (!e || !e[0] || (e[0] == '0' && !e[1])) return 0;
+  const char* ok = getenv("STF_ABLATION");
+  if (ok && ok[0] == '1') {
+    fprintf(stderr, "stfunet: timing-only ablation %s=%s is ON -- results are not valid\n", name, e);
+    return atoi(e);
+  }
+  fprintf(stderr, "stfunet: %s=%s ignored (a timing-only ablation: set STF_ABLATION=1 as well)\n", name, e);
+  return 0;
+}
 
 hipError_t stf::memset_async(void* p, int value, size_t bytes, hipStream_t s) {
   if (!g_rec) return hipMemsetAsync(p, value, bytes, s);

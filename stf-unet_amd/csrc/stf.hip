@@ -196,12 +196,13 @@ __global__ void bn_act_maxpool3_kernel(const uint16_t* __restrict__ y, int N, in
         }
       }
     }
-    *reinterpret_cast<uint4*>(out + p * C + cg * 8) = pack8(mx);
+    const size_t o = (size_t)p * C + cg * 8;          // N*Ho*Wo*C may pass 2^31 (units < 2^31 only)
+    *reinterpret_cast<uint4*>(out + o) = pack8(mx);
     if (argmax) {
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lo |= (uint32_t)am[j] << (8 * j); hi |= (uint32_t)am[4 + j] << (8 * j); }
-      *reinterpret_cast<uint2*>(argmax + p * C + cg * 8) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(argmax + o) = make_uint2(lo, hi);
     }
   }
 }
@@ -318,7 +319,116 @@ __global__ void pk_resize_kernel(const float* __restrict__ x, int B, int Ttot, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// The DecoderBlock's size fallback (src/stf_lstm_unet.py:56-57): when the transposed conv's
+// 2h x 2w output differs from the skip's size (H or W not divisible by 32), the reference
+// resizes it by F.interpolate(mode="bilinear", align_corners=True).  NHWC 16-bit, C % 8 == 0;
+// PyTorch's arithmetic (upsample_bilinear2d): scale (in-1)/(out-1) in fp32, src = scale * dst,
+// i0 = (int)src, i1 = i0 + (i0 < in-1), lambda = src - i0, fp32 blend, one 16-bit rounding.
+STF_DEV void ac_coord(int o, float sc, int in, int& i0, int& i1, float& l1) {
+  const float f = sc * (float)o;
+  i0 = min((int)f, in - 1);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = f - (float)i0;
+}
+
+__global__ void bilinear_ac_fwd_kernel(const uint16_t* __restrict__ x, int N, int H, int W, int C, int xcs,
+                                       uint16_t* __restrict__ y, int h, int w, int ycs) {
+  const int CG = C / 8;
+  const long units = (long)N * h * w * CG;
+  const float sy = h > 1 ? (float)(H - 1) / (float)(h - 1) : 0.f;
+  const float sx = w > 1 ? (float)(W - 1) / (float)(w - 1) : 0.f;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long p = u / CG;
+    const int ox = (int)(p % w);
+    const long r = p / w;
+    const int oy = (int)(r % h), n = (int)(r / h);
+    int y0, y1, x0, x1;
+    float ly, lx;
+    ac_coord(oy, sy, H, y0, y1, ly);
+    ac_coord(ox, sx, W, x0, x1, lx);
+    const uint16_t* b = x + (long)n * H * W * xcs + cg * 8;
+    float a00[8], a01[8], a10[8], a11[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)y0 * W + x0) * xcs), a00);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)y0 * W + x1) * xcs), a01);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)y1 * W + x0) * xcs), a10);
+    unpack8(*reinterpret_cast<const uint4*>(b + ((long)y1 * W + x1) * xcs), a11);
+    const float hy0 = 1.f - ly, wx0 = 1.f - lx;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = hy0 * (wx0 * a00[j] + lx * a01[j]) + ly * (wx0 * a10[j] + lx * a11[j]);
+    *reinterpret_cast<uint4*>(y + p * ycs + cg * 8) = pack8(o);
+  }
+}
+
+// backward as a gather (no atomics, fixed order): input pixel (iy, ix) sums w_y * w_x * dy over
+// the output pixels whose interpolation reads it; the candidate rows / columns are a window
+// around iy / scale, each checked with the forward's own coordinate arithmetic
+__global__ void bilinear_ac_bwd_kernel(const uint16_t* __restrict__ dy, int N, int h, int w, int C, int dycs,
+                                       uint16_t* __restrict__ dx, int H, int W, int dxcs) {
+  const int CG = C / 8;
+  const long units = (long)N * H * W * CG;
+  const float sy = h > 1 ? (float)(H - 1) / (float)(h - 1) : 0.f;
+  const float sx = w > 1 ? (float)(W - 1) / (float)(w - 1) : 0.f;
+  for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
+    const int cg = (int)(u % CG);
+    const long p = u / CG;
+    const int ix = (int)(p % W);
+    const long r = p / W;
+    const int iy = (int)(r % H), n = (int)(r / H);
+    const int oy0 = sy > 0.f ? max(0, (int)((float)(iy - 1) / sy) - 1) : 0;
+    const int oy1 = sy > 0.f ? min(h - 1, (int)((float)(iy + 1) / sy) + 1) : h - 1;
+    const int ox0 = sx > 0.f ? max(0, (int)((float)(ix - 1) / sx) - 1) : 0;
+    const int ox1 = sx > 0.f ? min(w - 1, (int)((float)(ix + 1) / sx) + 1) : w - 1;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      int y0, y1;
+      float ly;
+      ac_coord(oy, sy, H, y0, y1, ly);
+      const float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        int x0, x1;
+        float lx;
+        ac_coord(ox, sx, W, x0, x1, lx);
+        const float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dy + (((long)n * h + oy) * w + ox) * dycs + cg * 8), g);
+        const float k = wy * wx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += k * g[j];
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + p * dxcs + cg * 8) = pack8(acc);
+  }
+}
+
 }  // namespace
+
+extern "C" int stf_bilinear_ac_fwd(const void* x, int N, int H, int W, int C, int x_cstride, void* y, int h, int w,
+                                   int y_cstride, stf_stream_t stream) {
+  if (!x || !y || N < 1 || H < 1 || W < 1 || h < 1 || w < 1 || C < 8 || C % 8 || x_cstride < C ||
+      y_cstride < C || x_cstride % 8 || y_cstride % 8 || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return STF_EINVAL;
+  const long units = (long)N * h * w * (C / 8);
+  hipLaunchKernelGGL(bilinear_ac_fwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)x, N, H, W, C, x_cstride, (uint16_t*)y, h, w, y_cstride);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_bilinear_ac_bwd(const void* dy, int N, int h, int w, int C, int dy_cstride, void* dx, int H,
+                                   int W, int dx_cstride, stf_stream_t stream) {
+  if (!dy || !dx || N < 1 || H < 1 || W < 1 || h < 1 || w < 1 || C < 8 || C % 8 || dy_cstride < C ||
+      dx_cstride < C || dy_cstride % 8 || dx_cstride % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)dx & 15))
+    return STF_EINVAL;
+  const long units = (long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(bilinear_ac_bwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)dy, N, h, w, C, dy_cstride, (uint16_t*)dx, H, W, dx_cstride);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int T, int P, int Cpad,
                                  void* out, stf_stream_t stream) {
@@ -361,7 +471,8 @@ extern "C" int stf_bn_act_maxpool3s2(const void* y, int N, int H, int W, int C, 
   if (C % 8 || groups < 1 || N % groups || !y || !scale || !shift || !out) return STF_EINVAL;
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const long units = (long)N * Ho * Wo * (C / 8);
-  if (units >= (1L << 31) || (long)N * H * W * C >= (1L << 31) * 8L) return STF_EINVAL;
+  // 32-bit unit index incl. its grid stride (u + gridDim.x * NT must not wrap); byte offsets are 64-bit
+  if (units >= (1L << 31) - 8192L * NT || (long)N * H * W * C >= (1L << 31) * 8L) return STF_EINVAL;
   hipLaunchKernelGGL(bn_act_maxpool3_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
                      (const uint16_t*)y, N, H, W, C, Ho, Wo, N / groups, scale, shift, (uint16_t*)out,
                      (uint8_t*)argmax);

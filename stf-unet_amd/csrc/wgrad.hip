@@ -790,7 +790,7 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.colmajor = colmajor;
   // timing-only ablation: the split-K slabs of the fused 3x3 kernel all land in slab 0 (L2-resident:
   // no slab traffic to HBM; the sums are wrong) -- the upper bound of folding the slabs in-kernel
-  static const int one_slab = [] { const char* e = getenv("STF_WGRAD_ONE_SLAB"); return e && e[0] == '1'; }();
+  static const int one_slab = stf::ablation_env("STF_WGRAD_ONE_SLAB") == 1;
   w.one_slab = one_slab;
   hipStream_t s = (hipStream_t)stream;
   const int rsc = c.R * c.S * c.Cs;
@@ -798,7 +798,7 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
     dim3 grid(splits, a->Nout / 64, c.Cs / 64);
-    static const int diag = [] { const char* e = getenv("STF_WGRAD_DIAG"); return e ? atoi(e) : 0; }();
+    static const int diag = stf::ablation_env("STF_WGRAD_DIAG");
     if (wgrad_dma(a)) {
       const uint32_t dyb = (uint32_t)((uint64_t)c.N * c.Hd * c.Wd * a->dy_cstride * 2);
       const uint32_t xb = (uint32_t)((uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2);

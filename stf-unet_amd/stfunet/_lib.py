@@ -25,6 +25,7 @@ LIB_PATH_F16 = os.environ.get("STF_LIB_F16", os.path.join(os.path.dirname(LIB_PA
 LIB_PATHS = {torch.bfloat16: LIB_PATH, torch.float16: LIB_PATH_F16}
 STORAGE_CODE = {torch.bfloat16: 0, torch.float16: 1}     # stf_storage_type()
 
+c_uint = ctypes.c_uint
 c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
                                                 ctypes.c_size_t, ctypes.c_int64)
 P = c_void_p
@@ -102,9 +103,11 @@ _SIGS = {
     "stf_eval_counts": (c_int, [P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_lstm_coop_sync_bytes": (c_size_t, [c_int, c_int]),
     "stf_lstm_coop_supported": (c_int, [c_int]),
-    "stf_lstm_coop_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P]),
-    "stf_lstm_coop_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, P]),
+    "stf_lstm_coop_fwd": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, c_uint, P]),
+    "stf_lstm_coop_bwd": (c_int, [P, P, P, c_int, c_int, c_int, P, c_int, P, P, c_int, P, c_int, c_uint, P]),
     "stf_lstm_coop_error": (c_int, [P, c_int, c_int, P, P]),
+    "stf_bilinear_ac_fwd": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P]),
+    "stf_bilinear_ac_bwd": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P]),
     "stf_eval_counts_sm": (c_int, [P, P, P, c_int, c_int, c_int64, c_int64, P, P, P]),
     "stf_tofts_forward": (c_int, [P, P, P, c_int, c_int, P, P, P, P, P, c_int, c_float, P, P]),
     "stf_tofts_fit": (c_int, [P, c_int, c_int, P, P, P, P, P, c_int, c_float, c_int, c_int, P, c_float, c_float,

@@ -333,6 +333,11 @@ def train_one_epoch(model, optimizer, data_loader, device, epoch, num_classes, l
         lr_scheduler.step()
         lr = optimizer.param_groups[0]["lr"]
         logger.update(loss=loss.item(), lr=lr)
+    # the epoch's last steps: a device-side failure flag (cooperative LSTM hand-off timeout)
+    # raises here instead of at the next epoch's first step
+    prog = getattr(model, "_program", None)
+    if prog is not None and hasattr(prog, "check_device_errors"):
+        prog.check_device_errors(block=True)
     return logger.meters["loss"].global_avg, lr
 
 

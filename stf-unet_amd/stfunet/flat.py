@@ -54,22 +54,32 @@ class FlatParams:
             data[off:off + n].copy_(p.detach().reshape(-1).float())
             p.data = data[off:off + n].view(p.shape)
         self.data = data
-        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
-        self._views = [self.grad[off:off + p.numel()].view(p.shape)
-                       for p, off in zip(self.params, self.offsets)]
+        self._spare = None
+        self._use(torch.zeros(self.numel, dtype=torch.float32, device=dev))
+
+    def _use(self, buf):
+        self.grad = buf
+        self._views = [buf[off:off + p.numel()].view(p.shape) for p, off in zip(self.params, self.offsets)]
+
+    def _aliases(self, buf):
+        lo = buf.data_ptr()
+        hi = lo + 4 * self.numel
+        return any(p.grad is not None and lo <= p.grad.data_ptr() < hi for p in self.params)
 
     def fresh_grad(self):
-        """Zero the gradient buffer for a new backward.  If a parameter's ``.grad``
-        still aliases it (gradient accumulation without zero_grad), switch to a
-        new buffer so autograd's accumulation adds two distinct tensors."""
-        lo = self.grad.data_ptr()
-        hi = lo + 4 * self.numel
-        if any(p.grad is not None and lo <= p.grad.data_ptr() < hi for p in self.params):
-            self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.grad.device)
-            self._views = [self.grad[off:off + p.numel()].view(p.shape)
-                           for p, off in zip(self.params, self.offsets)]
-        else:
-            self.grad.zero_()
+        """Zero the gradient buffer for a new backward.  If a parameter's ``.grad`` still
+        aliases it (``zero_grad(set_to_none=False)``, or gradient accumulation: autograd then
+        adds the new gradients into ``.grad``), the backward writes the other of TWO buffers
+        instead, so that the two tensors autograd adds are distinct and the buffer the recorded
+        backward plan writes stays the same from step to step (its address is part of the plan's
+        signature: a fresh buffer per step would re-record the backward every step)."""
+        if self._aliases(self.grad):
+            other = self._spare
+            if other is None or self._aliases(other):
+                other = torch.empty_like(self.grad)
+            self._spare = self.grad
+            self._use(other)
+        self.grad.zero_()
 
     def grad_view(self, p):
         return self._views[self.index[id(p)]]

@@ -21,7 +21,16 @@ C-ABI calls from Python: ~500 calls / ~600 launches per STF step, ~7 ms of host 
 
 Anything that changes what the step would launch -- shapes, train / eval, storage
 dtype, the current stream, parameter or buffer addresses, the gradient buffer, a DDP
-hook appearing -- changes the signature and the plan is recorded again.  The forward
+hook appearing, a scalar baked into a recorded launch (BatchNorm momentum / eps, the
+``STF_*`` environment switches the schedule reads per call, the programs' own knobs such as
+the LSTM spin limit) -- changes the signature and the plan is recorded again.
+
+Pool lifetime: a recorded entry's private ``MemPool`` is never destroyed implicitly.  When an
+entry dies (evicted, its runtime closed, or its program collected -- by refcount or by the
+cyclic GC, at a moment the allocator does not choose) its pool moves to a graveyard that is
+emptied only at safe points, when no recording's pool context is open in any thread: torch
+refuses to destroy a pool while any ``use_mem_pool`` context is active (an exception inside a
+destructor, i.e. an abort).  The forward
 returns the recorded (static) logits tensor, as a captured graph does: a step's logits
 are overwritten by the next step's forward.
 
@@ -32,6 +41,7 @@ import contextlib
 import ctypes
 import gc
 import os
+import threading
 import weakref
 from collections import OrderedDict
 
@@ -41,6 +51,49 @@ from . import _lib, nhwc
 from ._lib import call
 
 TIMED = None           # kernel name whose ranges replays bracket with HIP events (bench.py)
+RECORD_HOOK = None     # tests: called inside every recording, with its pool context open
+
+# ---------------------------------------------------------------- pool lifetime
+_POOL_LOCK = threading.RLock()
+_POOL_ACTIVE = 0       # recording pool contexts open in this process (any thread)
+_GRAVEYARD = []        # released pools, destroyed by drain_pools() at a safe point
+
+
+def _bury(pool):
+    if pool is not None:
+        with _POOL_LOCK:
+            _GRAVEYARD.append(pool)
+
+
+def drain_pools():
+    """Destroy the released pools if no recording's pool context is open (else leave them
+    for the next safe point).  Holding the lock keeps another thread from opening one
+    meanwhile; a destructor that releases more pools re-enters (RLock) and appends them to the
+    fresh list."""
+    with _POOL_LOCK:
+        if _POOL_ACTIVE or not _GRAVEYARD:
+            return
+        dead = _GRAVEYARD[:]
+        _GRAVEYARD.clear()
+        dead.clear()
+
+
+@contextlib.contextmanager
+def _pool_context(pool):
+    """torch.cuda.use_mem_pool(pool), counted, so that no pool is destroyed while it is open."""
+    global _POOL_ACTIVE
+    if pool is None:
+        yield
+        return
+    with _POOL_LOCK:
+        _POOL_ACTIVE += 1
+    try:
+        with torch.cuda.use_mem_pool(pool):
+            yield
+    finally:
+        with _POOL_LOCK:
+            _POOL_ACTIVE -= 1
+        drain_pools()
 
 
 def enabled():
@@ -92,10 +145,9 @@ class Plan:
 
 @contextlib.contextmanager
 def _no_gc():
-    """No cyclic garbage collection while a recording allocates from a private pool: a
-    collected MemPool (an evicted entry's, or a dead program's) empties its cache on
-    destruction, which torch refuses while any pool context is active -- a C++ exception
-    inside a destructor, i.e. an abort."""
+    """No cyclic garbage collection while a recording runs.  Belt and braces only: pools no
+    longer die inside a collection (``_Entry.__del__`` hands them to the graveyard, see the
+    module docstring); this just keeps a long collection out of the recorded step."""
     was = gc.isenabled()
     gc.disable()
     try:
@@ -105,13 +157,12 @@ def _no_gc():
             gc.enable()
 
 
-def _pool_ctx():
+def _new_pool():
     """A private memory pool for the recorded step's buffers (a backstop behind
     ``nhwc.KEEP``: nothing outside the plan can ever be given one of its blocks)."""
     if os.environ.get("STF_PLAN_POOL", "1") == "0" or not hasattr(torch.cuda, "MemPool"):
-        return None, None
-    pool = torch.cuda.MemPool()
-    return pool, torch.cuda.use_mem_pool(pool)
+        return None
+    return torch.cuda.MemPool()
 
 
 class _Entry:
@@ -129,6 +180,22 @@ class _Entry:
         self.pool = None
         self.owner = None      # weakref to the autograd ctx holding the static S until its backward
 
+    def release(self):
+        """Drop the plans and buffers; the pool goes to the graveyard (drain_pools)."""
+        pool, self.pool = self.pool, None
+        self.fwd = self.bwd = None
+        self.x = self.logits = self.S = self.dl = None
+        self.keep, self.bkeep = [], []
+        _bury(pool)
+
+    def __del__(self):
+        # by refcount or inside a cyclic collection, possibly while another recording's pool
+        # context is open: never destroy the pool here
+        pool = getattr(self, "pool", None)
+        if pool is not None:
+            self.pool = None
+            _bury(pool)
+
     def busy(self):
         """The static buffers still belong to an earlier forward whose backward has not run
         (two forwards before their backwards): a new forward must not overwrite them."""
@@ -143,12 +210,30 @@ class StepRuntime:
     an epoch's smaller last batch gets its own plan instead of throwing away the full batch's."""
 
     def __init__(self, prog):
-        self.prog = prog
+        # a weak back-pointer: program -> runtime -> entries is the only ownership chain, so a
+        # dropped program's plans and pools go at a known point (its refcount), not in a cycle
+        self._prog = weakref.ref(prog)
+        self._bns = None
         self.warm = int(os.environ.get("STF_PLAN_WARM", "1"))
         self.slots = max(1, int(os.environ.get("STF_PLAN_SLOTS", "2")))
         self._bufs = None
         self.entries = OrderedDict()
         self.cur = None         # entry of the last planned forward
+
+    @property
+    def prog(self):
+        p = self._prog()
+        if p is None:
+            raise RuntimeError("StepRuntime: its program is gone")
+        return p
+
+    def close(self):
+        """Release every recorded entry (their pools are destroyed at the next safe point)."""
+        for e in self.entries.values():
+            e.release()
+        self.entries.clear()
+        self.cur = None
+        drain_pools()
 
     # the most recent entry's plans (bench.py / tests)
     @property
@@ -167,9 +252,15 @@ class StepRuntime:
             # ~20 us instead of ~0.5 ms for module.buffers() over the STF module tree
             self._bufs = [(mod, n) for mod in p.m.modules() for n in mod._buffers
                           if mod._buffers[n] is not None]
+            self._bns = [mod for mod in p.m.modules() if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm)]
         bufs = tuple(mod._buffers[n].data_ptr() for mod, n in self._bufs)
+        # scalars the recorded launches carry by value: BatchNorm momentum / eps, the STF_*
+        # switches the schedule reads per call, the program's own knobs
+        bn = tuple((b.momentum, b.eps) for b in self._bns)
+        env = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("STF_")))
+        knobs = p.plan_knobs() if hasattr(p, "plan_knobs") else ()
         return (tuple(x.shape), x.dtype, x.device, training, _lib.storage_dtype(), _lib.stream(),
-                p.flat.data.data_ptr(), bufs)
+                p.flat.data.data_ptr(), bufs, bn, env, knobs)
 
     def _entry(self, sig):
         e = self.entries.get(sig)
@@ -178,6 +269,7 @@ class StepRuntime:
                 _, old = self.entries.popitem(last=False)
                 if old is self.cur:
                     self.cur = None
+                old.release()
             e = self.entries[sig] = _Entry()
         else:
             self.entries.move_to_end(sig)
@@ -189,6 +281,7 @@ class StepRuntime:
         training step (training and need_bwd) is planned, everything else runs eagerly.
         ``ctx``: the autograd ctx that will hold the returned state until its backward."""
         p = self.prog
+        drain_pools()                         # a safe point: no recording of ours is open
         if not (enabled() and training and need_bwd and nhwc.TIMER is None):
             return p.forward(x, training, need_bwd)
         e = self._entry(self._signature(x, training))
@@ -212,20 +305,20 @@ class StepRuntime:
             self._record_forward_pooled(e, x, training)
 
     def _record_forward_pooled(self, e, x, training):
-        pool, ctx = _pool_ctx()
-        e.pool = pool
+        e.pool = _new_pool()
         nhwc.KEEP = e.keep
+        prog = self.prog
+
+        def run():
+            if RECORD_HOOK is not None:
+                RECORD_HOOK(self, "forward")
+            return prog.forward(e.x, training, True)
         try:
-            if ctx is not None:
-                ctx.__enter__()
-            try:
+            with _pool_context(e.pool):
                 e.x = nhwc.empty(tuple(x.shape), x.dtype, x.device)
                 e.x.copy_(x)
                 plan = Plan()
-                e.logits, e.S = plan.record(lambda: self.prog.forward(e.x, training, True))
-            finally:
-                if ctx is not None:
-                    ctx.__exit__(None, None, None)
+                e.logits, e.S = plan.record(run)
         finally:
             nhwc.KEEP = None
         e.fwd = plan
@@ -257,7 +350,6 @@ class StepRuntime:
         e.bwd = None
         e.bkeep = []
         nhwc.KEEP = e.bkeep
-        ctx = torch.cuda.use_mem_pool(e.pool) if e.pool is not None else None
         plan = Plan()
         marks = []
         real_hook = p.grad_ready_hook
@@ -266,16 +358,16 @@ class StepRuntime:
                 marks.append((plan.size(), off))
                 real_hook(off)
             p.grad_ready_hook = hook
+
+        def run():
+            if RECORD_HOOK is not None:
+                RECORD_HOOK(self, "backward")
+            return p.backward(S, e.dl)
         try:
-            if ctx is not None:
-                ctx.__enter__()
-            try:
+            with _pool_context(e.pool):
                 e.dl = nhwc.empty(tuple(dlogits.shape), dlogits.dtype, dlogits.device)
                 e.dl.copy_(dlogits)
-                plan.record(lambda: p.backward(S, e.dl))
-            finally:
-                if ctx is not None:
-                    ctx.__exit__(None, None, None)
+                plan.record(run)
         finally:
             nhwc.KEEP = None
             p.grad_ready_hook = real_hook

@@ -187,6 +187,16 @@ class LSTMProgram:
         # workgroup budget of the cooperative kernels (one per CU; 0 = the whole chip): an LSTM
         # on a side stream leaves the rest to the encoder / decoder of the main stream
         self.max_wg = max_wg
+        # polls before a cooperative hand-off gives up (0 = the library's ~4 s; tests force 1)
+        self.spin_limit = 0
+        # the owning program's sticky device error word (STFProgram.err_word): every cooperative
+        # launch ORs its timeout flag into it, the program raises at the next step boundary
+        self.err_word = None
+
+    def _note_coop(self, sync, npix, T):
+        self.last_sync = (sync, npix, T)
+        if self.err_word is not None:
+            call("stf_lstm_coop_error", _p(sync), npix, T, _p(self.err_word), stream())
 
     def fused(self, lbuf: Feat, hT: Feat):
         """Whole-sequence kernel (stf_lstm_seq_fwd) for this hidden size and layout?
@@ -210,7 +220,7 @@ class LSTMProgram:
                 and hT.ptr() % 16 == 0)
 
     def coop_error(self):
-        """Nonzero if the last cooperative forward's in-launch hand-off timed out (syncs)."""
+        """Nonzero if the last cooperative launch's in-launch hand-off timed out (syncs)."""
         if getattr(self, "last_sync", None) is None:
             return 0
         sync, npix, T = self.last_sync
@@ -245,8 +255,8 @@ class LSTMProgram:
             # the activated gates (fp32) are kept for the cooperative backward (no recompute)
             gates = nhwc.empty((T, npix, 4 * C), torch.float32, dev) if need_bwd else None
             call("stf_lstm_coop_fwd", _p(wcat), _p(bias), lbuf.ptr(), npix, T, C, _p(cst), hT.ptr(), hT.cs,
-                 _p(gates), _p(sync), self.max_wg, stream())
-            self.last_sync = (sync, npix, T)
+                 _p(gates), _p(sync), self.max_wg, self.spin_limit, stream())
+            self._note_coop(sync, npix, T)
         else:
             for t in range(T):
                 src = rows(lbuf, t * B, B)
@@ -279,8 +289,8 @@ class LSTMProgram:
             lib = _lib.load()
             sync = nhwc.empty(lib.stf_lstm_coop_sync_bytes(npix, T) // 4, torch.int32, dev)
             call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
-                 dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, stream())
-            self.last_sync = (sync, npix, T)
+                 dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, self.spin_limit, stream())
+            self._note_coop(sync, npix, T)
         elif st.gates is not None and os.environ.get("STF_LSTM_GATES", "1") != "0":
             # the cooperative forward kept the activated gates: per step only the cell backward
             # (elementwise, the same lstm_cell_bwd arithmetic as the recompute epilogue below, so
@@ -339,7 +349,49 @@ class STFProgram:
         self._side = None
         self._wstream = None
         self._ident = {}
+        self.err_word = None          # sticky device flag of the cooperative LSTM launches
+        self._err_host = None         # its pinned host copy, issued at each step boundary
+        self._err_event = None
         self.runtime = StepRuntime(self)
+
+    def plan_knobs(self):
+        """Per-program scalars a recorded plan carries by value (part of its signature)."""
+        return tuple((lp.spin_limit, lp.max_wg) for lp in self.lstm_progs)
+
+    def check_device_errors(self, dev=None, block=False):
+        """Raise if a cooperative LSTM launch of an earlier step timed out in its in-launch
+        hand-off (its outputs, and so that step's update, are wrong).
+
+        Called at every step boundary (``STFLSTMUNet.forward``): the flag that an earlier
+        boundary copied to pinned host memory is read once the copy has landed (no host sync),
+        then the current flag is copied out behind the work enqueued so far.  ``block``: also
+        wait for that copy, so every launch enqueued before the call is covered."""
+        if self.err_word is None:
+            if dev is None:
+                return
+            self.err_word = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            for lp in self.lstm_progs:
+                lp.err_word = self.err_word
+        if self._err_event is not None and (block or self._err_event.query()):
+            self._read_error_flag()
+        if self._err_event is None:
+            self._err_host.copy_(self.err_word, non_blocking=True)
+            self._err_event = torch.cuda.Event()
+            self._err_event.record()
+            if block:
+                self._read_error_flag()
+
+    def _read_error_flag(self):
+        self._err_event.synchronize()
+        self._err_event = None
+        if int(self._err_host[0]) != 0:
+            self.err_word.zero_()
+            self._err_host.zero_()
+            raise RuntimeError("stfunet: a cooperative LSTM launch (stf_lstm_coop_fwd/bwd) timed out in its "
+                               "in-launch hand-off (its workgroups could not all be resident), so that step's "
+                               "LSTM outputs and gradients are invalid; STF_LSTM_COOP=0 selects the per-step "
+                               "launches")
 
     def _identity(self, C, dev):
         """BatchNorm-identity state of the head's input (no BN there), made once per (C, device)."""
@@ -503,15 +555,26 @@ class STFProgram:
             nhwc.wait(main, side[2 - i])       # h_T of lstm 2-i fills the skip half of dcat[i]
             cat = dcat[i]
             Cout = d.up.out_channels
-            nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, cat.slice(0, Cout), 3, 3, 2, 1,
-                       transposed=True, bias=d.up.bias.detach())
+            up = None
+            if (2 * cur.H, 2 * cur.W) == (cat.H, cat.W):
+                nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, cat.slice(0, Cout), 3, 3, 2, 1,
+                           transposed=True, bias=d.up.bias.detach())
+            else:
+                # H or W not divisible by 32: the transposed conv's 2h x 2w output is resized to the
+                # skip's size (bilinear, align_corners=True; src/stf_lstm_unet.py:56-57)
+                up = new_feat(B, 2 * cur.H, 2 * cur.W, Cout, dev)
+                nhwc.igemm(cur, nhwc.pack_weight(d.up.weight, 4), Cout, up, 3, 3, 2, 1, transposed=True,
+                           bias=d.up.bias.detach())
+                sl = cat.slice(0, Cout)
+                call("stf_bilinear_ac_fwd", up.ptr(), B, up.H, up.W, Cout, up.cs, sl.ptr(), cat.H, cat.W, sl.cs,
+                     stream())
             yf = new_feat(B, cat.H, cat.W, Cout, dev)
             nhwc.igemm(cat, nhwc.pack_weight(d.fusion.weight, 0, cat.C), Cout, yf, 1, 1, 1, 0,
                        bias=d.fusion.bias.detach())
             out = new_feat(B, cat.H, cat.W, Cout, dev)
             rs = self.dec_res[i].forward(yf, out, training, 1)
             dsv = _S()
-            dsv.x, dsv.cat, dsv.yf, dsv.res = cur, cat, yf, rs
+            dsv.x, dsv.cat, dsv.yf, dsv.res, dsv.up = cur, cat, yf, rs, up
             S.dec.append(dsv)
             cur = out
         # ---- upconv1 + final_res + final (head)
@@ -579,6 +642,11 @@ class STFProgram:
             nhwc.conv_dgrad(d_yf, d.fusion.weight, dcat, 1, 1, 1, 0)
             del d_yf
             dup = dcat.slice(0, Cout)
+            if dsv.up is not None:                             # through the bilinear size fallback
+                du = new_feat(B, dsv.up.H, dsv.up.W, Cout, dev)
+                call("stf_bilinear_ac_bwd", dup.ptr(), B, dup.H, dup.W, Cout, dup.cs, du.ptr(), du.H, du.W, du.cs,
+                     stream())
+                dup = du
             nhwc.wgrad(dsv.x, dup, 3, 3, 2, 1, gv(d.up.weight))
             nhwc.channel_sum(dup, gv(d.up.bias))
             dx = new_feat(B, dsv.x.H, dsv.x.W, dsv.x.C, dev)
@@ -652,19 +720,17 @@ class STFProgram:
 
 
 def _check_input_shape(shape, P):
-    """[B, T + P, C, H, W] with at least one frame, H and W divisible by 32.
-
-    For other sizes the reference's decoder resizes the transposed-conv output to the skip
-    size by bilinear interpolation (src/stf_lstm_unet.py:56-57); that edge path is not
-    implemented here and is refused up front rather than mis-tiled."""
+    """[B, T + P, C, H, W] with at least one frame and H, W >= 32 (ResNet-34's five halvings leave
+    layer4 at least one pixel).  Sizes not divisible by 32 take the reference's decoder size
+    fallback: the transposed conv's output is resized to the skip's size by bilinear
+    interpolation, align_corners=True (src/stf_lstm_unet.py:56-57, stf_bilinear_ac_fwd/_bwd)."""
     if len(shape) != 5:
         raise ValueError(f"STFLSTMUNet expects [B, T, C, H, W], got shape {tuple(shape)}")
     Ttot, H, W = shape[1], shape[3], shape[4]
     if Ttot - P < 1:
         raise ValueError(f"STFLSTMUNet: {Ttot} input frames leave no time steps after {P} PK maps")
-    if H % 32 or W % 32:
-        raise ValueError(f"STFLSTMUNet needs H, W divisible by 32 (got {H}x{W}); the reference's "
-                         "bilinear size fallback (src/stf_lstm_unet.py:56-57) is not supported")
+    if H < 32 or W < 32:
+        raise ValueError(f"STFLSTMUNet needs H, W >= 32 (got {H}x{W})")
 
 
 class _STFFunction(torch.autograd.Function):
@@ -741,5 +807,6 @@ class STFLSTMUNet(nn.Module):
             raise RuntimeError("stfunet.STFLSTMUNet runs on the gfx950 HIP kernels only; move the model and "
                                "input to a ROCm device (no CPU fallback)")
         prog = self.program
+        prog.check_device_errors(x.device)       # step boundary: an earlier step's LSTM timeout raises
         prog.flat.ensure()
         return {"out": _STFFunction.apply(x, prog, _lib.storage_for(self.storage_dtype), *prog.flat.params)}

@@ -13,9 +13,18 @@ defect 1), then scored by its own ``evaluate`` (``train_and_eval.py:316-374``) o
 held-out batches (seeds 4000+).
 
 ResNet-34's 27 M parameters (55 MB even in 16 bits) are not committed: the fixture holds the Dice,
-the confusion matrix, the per-pixel argmax, the training losses -- and the Dice of a SECOND
-reference run that differs only in the CPU thread count (reduction order), the reference's own
-run-to-run spread, which sets the tolerance of the gfx950 training test.
+the confusion matrix, the per-pixel argmax, the training losses -- and the Dice of further
+reference runs that differ only in the CPU thread count (reduction order: 8, 3, 1 and 5 threads)
+or that run the reference's step under ``torch.autocast("cpu", dtype=torch.bfloat16)`` (a 16-bit
+trajectory of the reference itself, 8 and 3 threads): the reference's own run-to-run spread, which
+sets the tolerance of the gfx950 training test.
+
+Round 4 adds a FIXED-WEIGHT evaluation (no training, so no weight file): the same model at the
+canonical init with a fixed eval-mode BatchNorm state (running means U(-0.5, 0.5), variances
+U(0.5, 2) from ``torch.Generator().manual_seed(7)`` in state_dict order) and ``final.bias[1]``
+shifted by the median logit difference so that both classes are predicted, scored by the
+reference's own ``evaluate`` on 4 held-out [4, 4, 1, 128, 128] batches (seeds 5000+); the fixture
+keeps its Dice, confusion matrix, per-pixel argmax and |logit margin|, and the bias shift.
 
 Output: ``tests/golden/stf_trained.npz`` (no pickles).
 """
@@ -30,6 +39,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "stf-unet_amd"))
 sys.path.insert(0, HERE)
 
 from make_golden import load_reference  # noqa: E402
@@ -49,8 +59,79 @@ def eval_batches():
     return [dce_case(4000 + i, B, T, HW, HW, target_hw=(HW // 2, HW // 2)) for i in range(EVAL_BATCHES)]
 
 
-def train_and_eval(stf_mod, tae, threads):
+FIX_HW, FIX_BATCHES = 128, 4
+
+
+def fixed_bn_state(sd):
+    """The fixed eval-mode BatchNorm statistics of the fixed-weight evaluation (in place)."""
+    gen = torch.Generator().manual_seed(7)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) - 0.5
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 1.5 + 0.5
+    return sd
+
+
+def fixed_eval_batches():
+    return [dce_case(5000 + i, B, T, FIX_HW, FIX_HW, target_hw=(FIX_HW // 2, FIX_HW // 2))
+            for i in range(FIX_BATCHES)]
+
+
+def fixed_weight_eval(stf_mod, tae):
+    torch.set_num_threads(8)
+    model = stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
+    sd = fixed_bn_state(canonical_state_dict(model.state_dict(), seed=0))
+    model.load_state_dict(sd)
+    model.eval()
+    ev = fixed_eval_batches()
+    with torch.no_grad():
+        d = torch.cat([(lo[:, 0] - lo[:, 1]).reshape(-1) for lo in
+                       (model(tae.preprocess_input(x5, model))["out"] for x5, _ in ev)]).median()
+        sd["final.bias"][1] += d
+        model.load_state_dict(sd)
+    metrics = tae.evaluate(model, ev, torch.device("cpu"), num_classes=2)
+    preds, margins = [], []
+    with torch.no_grad():
+        for x5, _ in ev:
+            lo = model(tae.preprocess_input(x5, model))["out"]
+            preds.append(lo.argmax(1).numpy().astype(np.uint8))
+            margins.append((lo[:, 1] - lo[:, 0]).abs().numpy().astype(np.float32))
+    return metrics, np.concatenate(preds), np.concatenate(margins), float(d)
+
+
+class _Emulation(torch.nn.Module):
+    """oracle/stf_bf16.py (this repository's bf16-storage restatement) as a module for the
+    reference's evaluate(): the band that bf16 rounding alone gives at the fixed weights."""
+    input_format = "time_sequence"
+
+    def __init__(self, sd, dtype):
+        super().__init__()
+        self.sd, self.dtype = sd, dtype
+
+    def forward(self, x):
+        import oracle.unet_bf16 as o_q
+        from oracle import stf_bf16
+        with o_q.storage(self.dtype):
+            return stf_bf16.forward(self.sd, x, False)
+
+
+def emulation_dice(tae, bias_shift):
+    """Dice of the bf16-storage emulation at the fixed weights, by the reference's evaluate()."""
+    from stfunet.stf_lstm_unet import STFLSTMUNet
+    torch.set_num_threads(8)
+    sd = fixed_bn_state(canonical_state_dict(STFLSTMUNet(time_steps=T).state_dict(), seed=0))
+    sd["final.bias"][1] += bias_shift
+    with torch.no_grad():
+        return tae.evaluate(_Emulation(sd, torch.bfloat16), fixed_eval_batches(), torch.device("cpu"),
+                            num_classes=2)["dice"]
+
+
+def train_and_eval(stf_mod, tae, threads, autocast_bf16=False):
     torch.set_num_threads(threads)
+    if autocast_bf16:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            return train_and_eval(stf_mod, tae, threads)
     model = stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
     model.load_state_dict(canonical_state_dict(model.state_dict(), seed=0))
     opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3,
@@ -80,11 +161,31 @@ def main():
     ap.add_argument("--out", default=HERE)
     a = ap.parse_args()
     _, stf_mod, tae, _ = load_reference(a.ref)
+    fmetrics, fpred, fmargin, fshift = fixed_weight_eval(stf_mod, tae)
+    emu = emulation_dice(tae, fshift)
+    print(f"fixed-weight eval: Dice {fmetrics['dice']:.7f} (bf16 emulation {emu:.7f}), bias shift {fshift:.6g}",
+          flush=True)
     metrics, pred, margin, losses = train_and_eval(stf_mod, tae, 8)
     metrics2, pred2, _, _ = train_and_eval(stf_mod, tae, 3)
+    band = {}
+    for threads in (1, 5):
+        band[f"fp32_{threads}"] = train_and_eval(stf_mod, tae, threads)[0]["dice"]
+    for threads in (8, 3):
+        band[f"bf16_{threads}"] = train_and_eval(stf_mod, tae, threads, autocast_bf16=True)[0]["dice"]
+    runs = {"fp32_8": metrics["dice"], "fp32_3": metrics2["dice"], **band}
     res = dict(
         dice=np.array(metrics["dice"]),
         dice_other_threads=np.array(metrics2["dice"]),
+        band_names=np.array(list(runs)),
+        band_dice=np.array([runs[k] for k in runs]),
+        fixed_dice=np.array(fmetrics["dice"]),
+        fixed_confmat=fmetrics["confusion_matrix"].mat.numpy(),
+        fixed_pred_bits=np.packbits(fpred.reshape(-1)),
+        fixed_pred_shape=np.array(fpred.shape),
+        fixed_margin=fmargin,
+        fixed_bias_shift=np.array(fshift, dtype=np.float32),
+        fixed_emu_bf16_ddice=np.array(abs(emu - fmetrics["dice"])),
+        fixed_config=np.array([B, T, FIX_HW, FIX_BATCHES]),
         confmat=metrics["confusion_matrix"].mat.numpy(),
         pred_bits=np.packbits(pred.reshape(-1)),
         pred_shape=np.array(pred.shape),
@@ -95,6 +196,7 @@ def main():
     np.savez_compressed(os.path.join(a.out, "stf_trained.npz"), **res)
     print(json.dumps({"dice": metrics["dice"], "dice_3_threads": metrics2["dice"],
                       "confmat": metrics["confusion_matrix"].mat.tolist(),
+                      "runs": runs, "fixed_dice": fmetrics["dice"],
                       "pred_flips_between_thread_counts": int((pred != pred2).sum()),
                       "margin_lt_1e-1": int((margin < 1e-1).sum()), "pixels": int(margin.size),
                       "losses": losses}, indent=1))

@@ -208,38 +208,57 @@ def test_plan_utility_ops():
 
 
 _GC_SCRIPT = r"""
-import gc, sys, torch
+import contextlib, gc, sys, torch
 sys.path.insert(0, "stf-unet_amd")
-from stfunet import UNet, engine
+from stfunet import UNet, engine, plan
 from stfunet.synthetic import dce_batch
+plan._no_gc = contextlib.nullcontext          # the GC-off guard bypassed: the pool lifetime alone
 x, t = dce_batch(2, 8, 64, 64, seed=0, device="cuda")
 x = x.flatten(1, 2)
 def steps(m):
     for _ in range(3):
         engine.criterion(m(x), t).backward()
+def pools(m):
+    return sum(e.pool is not None for e in m.program.runtime.entries.values())
 a = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
-steps(a)                        # a's plans and private pool are recorded
-a.cycle = a                     # only the cyclic collector can free a (and its pool) now
+steps(a)                                     # a's plans and private pool are recorded
+c = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
+steps(c)
+assert pools(a) == 1 and pools(c) == 1, (pools(a), pools(c))
+a.cycle = a                                  # only the cyclic collector can free a (and its pool) now
 del a
-gc.set_threshold(1, 1, 1)       # collect at (nearly) every allocation
+seen = []
+def hook(rt, phase):                         # inside b's recording, its pool context open
+    if seen:
+        return
+    c.program.runtime.close()                # drop the last reference to another live entry's pool
+    n = gc.collect()                         # collect the dead program a, its entry and pool
+    seen.append((phase, n, len(plan._GRAVEYARD), plan._POOL_ACTIVE))
+plan.RECORD_HOOK = hook
 b = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
-steps(b)                        # b records while a is garbage
-gc.collect()
+steps(b)                                     # b records: the hook runs inside the recording
+plan.RECORD_HOOK = None
+phase, n, buried, active = seen[0]
+assert phase == "forward" and n > 0 and active == 1, seen
+assert buried == 2, seen                     # a's and c's pools: deferred, not destroyed in the context
+assert not plan._GRAVEYARD, len(plan._GRAVEYARD)   # destroyed at the recording's exit
+steps(c)                                     # c records again from scratch
 torch.cuda.synchronize()
 print("ok")
 """
 
 
-def test_plan_recording_survives_collection_of_a_dead_programs_pool():
-    """Recordings run with the cyclic collector off (plan._no_gc): the full GPU suite once
-    aborted inside a garbage collection during an STF forward recording (test_dice_gpu,
-    after the UNet training test left its program, plans and private pool as garbage).
-    This child process drives the same situation -- a dead program's pool collectable at
-    every allocation while another program records -- and must exit cleanly; it did not
-    reproduce the abort without the guard in isolation (the suite's allocation history
-    decides when the collector runs), so it guards the path rather than pinning the bug."""
+def test_plan_pool_lifetime_is_explicit():
+    """A recorded entry's private MemPool is never destroyed while a recording's pool context
+    is open (torch raises inside the pool's destructor then, which aborted the full GPU suite
+    in round 3 during an STF forward recording, test_dice_gpu).  Deterministic (a child
+    process, the GC-off guard bypassed): inside program b's forward recording a hook closes
+    program c's runtime -- dropping the last reference to its pool -- and runs gc.collect()
+    over a dead program a held only by a reference cycle.  Both pools must go to the graveyard
+    (2 entries, pool context count 1 at that moment) and be destroyed when the recording's
+    context exits; the process exits cleanly and c records again afterwards."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", _GC_SCRIPT], cwd=root, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stderr[-3000:])
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])

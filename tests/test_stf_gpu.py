@@ -572,3 +572,116 @@ def test_stem_bn_backward_through_maxpool():
     torch.cuda.synchronize()
     assert rel(res["new"][0], res["old"][0]) < 5e-3
     assert rel(res["new"][1], res["old"][1]) < 1e-4 and rel(res["new"][2], res["old"][2]) < 1e-4
+
+
+def test_lstm_coop_timeout_raises(monkeypatch):
+    """A cooperative LSTM launch whose in-launch hand-off times out must not pass silently
+    (VERDICT r03 weak #6): the kernel sets its error word and drains, the launch ORs it into the
+    program's sticky device flag, and the next step boundary (forward) -- or the epoch's end,
+    block=True -- raises RuntimeError.  Forced with spin_limit 0xFFFFFFFF (every hand-off reports
+    a timeout at once); a normal step with the default limit never raises."""
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    monkeypatch.setenv("STF_LSTM_COOP", "512")
+    g = np.load(os.path.join(GOLDEN, "stf_t4.npz"))
+    x, t = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["target"]).to(DEV)
+    m = STFLSTMUNet(time_steps=4)
+    m.load_state_dict(canonical_state_dict(m.state_dict(), seed=0))
+    m = m.to(DEV).train()
+    for _ in range(2):
+        criterion(m(x), t).backward()
+    m.program.check_device_errors(block=True)                  # default limit: no timeout
+    lp = m.program.lstm_progs[3]
+    lp.spin_limit = 0xFFFFFFFF
+    out = m(x)
+    assert lp.coop_error() != 0                                 # the launch saw its hand-offs fail
+    criterion(out, t).backward()
+    lp.spin_limit = 0
+    with pytest.raises(RuntimeError, match="cooperative LSTM"):
+        m.program.check_device_errors(block=True)
+    m.program.check_device_errors(block=True)                  # flag cleared after the raise
+    lp.spin_limit = 0xFFFFFFFF
+    m(x)
+    lp.spin_limit = 0
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="cooperative LSTM"):
+        for _ in range(2):                                      # the copy issued at the boundary
+            m(x)                                                # lands; a later boundary raises
+            torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("H,W,h,w", [(14, 18, 13, 17), (6, 8, 5, 7), (7, 9, 13, 17), (1, 4, 3, 1)])
+def test_bilinear_align_corners_kernels(H, W, h, w):
+    """stf_bilinear_ac_fwd / _bwd (the DecoderBlock size fallback, src/stf_lstm_unet.py:56-57)
+    against F.interpolate(mode="bilinear", align_corners=True) and its autograd on the bf16 values
+    in fp32: down- and up-sizing, ragged sizes, a size-1 side; strided NHWC slices as in the
+    decoder (the output is the concat buffer's first channels).  bf16 outputs: rel-L2 <= 1e-2,
+    and the 16-bit rounding of each output is the only difference (max abs <= 1 bf16 ulp-ish)."""
+    from stfunet import _lib, nhwc
+    N, C = 3, 64
+    x = nhwc.new_feat(N, H, W, C + 8, DEV).slice(8, C)
+    x.buf.normal_()
+    y = nhwc.new_feat(N, h, w, 2 * C, DEV).slice(0, C)
+    _lib.call("stf_bilinear_ac_fwd", x.ptr(), N, H, W, C, x.cs, y.ptr(), h, w, y.cs, _lib.stream())
+    xr = x.dense().float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    ref = F.interpolate(xr, size=(h, w), mode="bilinear", align_corners=True)
+    got = y.dense().float().permute(0, 3, 1, 2)
+    assert rel(got, ref) <= 1e-2, rel(got, ref)
+    assert (got - ref.to(torch.bfloat16).float()).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    dy = nhwc.new_feat(N, h, w, C + 16, DEV).slice(16, C)
+    dy.buf.normal_()
+    dx = nhwc.new_feat(N, H, W, C, DEV)
+    _lib.call("stf_bilinear_ac_bwd", dy.ptr(), N, h, w, C, dy.cs, dx.ptr(), H, W, dx.cs, _lib.stream())
+    ref.backward(dy.dense().float().permute(0, 3, 1, 2))
+    gdx = dx.dense().float().permute(0, 3, 1, 2)
+    assert rel(gdx, xr.grad) <= 1e-2, rel(gdx, xr.grad)
+
+
+def test_stf_size_fallback_vs_oracle():
+    """H, W not divisible by 32 (72 x 104: layer4 is 3 x 4, so decoder4 and decoder3 resize their
+    transposed-conv outputs 6x8 -> 5x7 and 10x14 -> 9x13 to the skips; src/stf_lstm_unet.py:56-57):
+    whole-model logits in eval mode (fixed running statistics) within 2x the bf16 emulation's error
+    + 2e-3 of the fp32 restatement, and every parameter gradient of an eval-mode backward within 2x
+    the emulation's error + 0.02 (as test_stf_fullsize_eval_backward_vs_fp32)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    from stfunet.synthetic import dce_batch
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=3)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    gen = torch.Generator().manual_seed(5)
+    for k, v in sd.items():
+        if "running_mean" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.2 - 0.1
+        if "running_var" in k:
+            sd[k] = torch.rand(v.shape, generator=gen) * 0.5 + 0.75
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = dce_batch(2, 3, 72, 104, seed=12, device=DEV, mask_hw=(36, 52))
+    p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    ref = o_stf.forward(p, x, False)["out"]
+    ref_loss = o_loss.criterion(ref, t)
+    ref_loss.backward()
+    pe = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    with o_q.storage(torch.bfloat16):
+        emu = o_emu.forward(pe, x, False)["out"]
+        o_loss.criterion(emu, t).backward()
+    out = m(x)["out"]
+    assert out.shape == ref.shape == (2, 2, 36, 52)
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    assert e_hip <= 2 * e_emu + 2e-3, (e_hip, e_emu)
+    loss = criterion({"out": out}, t)
+    loss.backward()
+    assert abs(loss.item() - ref_loss.item()) < 1e-2, (loss.item(), ref_loss.item())
+    bad = []
+    for k, prm in m.named_parameters():
+        eh, ee = rel(prm.grad, p[k].grad), rel(pe[k].grad, p[k].grad)
+        if eh > 2 * ee + 0.02:
+            bad.append((k, eh, ee))
+    print(f"\nSTF 72x104 (size fallback): logits rel {e_hip:.3e} (emu {e_emu:.3e}), loss {loss.item():.6f} vs "
+          f"{ref_loss.item():.6f}")
+    assert not bad, bad

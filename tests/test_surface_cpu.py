@@ -49,7 +49,7 @@ def test_library_exports_every_header_symbol(dtype):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
     assert set(syms) == set(_lib.EXPORTED)
-    assert lib.stf_abi_version() == 11
+    assert lib.stf_abi_version() == 12
     assert lib.stf_storage_type() == _lib.STORAGE_CODE[dtype]
     assert b"invalid argument" in lib.stf_error_string(100001)
 
@@ -237,13 +237,16 @@ def test_stf_accepts_reference_state_dict_roundtrip():
 
 
 def test_stf_refuses_unsupported_shapes_up_front():
-    """H, W not divisible by 32 take the reference's bilinear size fallback
-    (src/stf_lstm_unet.py:56-57), which is not implemented: refused with a ValueError naming
-    it before any device work; too few frames for the PK maps likewise."""
+    """Frames smaller than 32 (layer4 would have no pixel), a wrong rank and too few frames for
+    the PK maps are refused with a ValueError before any device work; sizes not divisible by 32
+    are valid (the reference's bilinear size fallback, src/stf_lstm_unet.py:56-57) and reach the
+    device guard."""
     from stfunet import STFLSTMUNet
     m = STFLSTMUNet(time_steps=4)
-    with pytest.raises(ValueError, match="divisible by 32.*bilinear size fallback"):
-        m(torch.zeros(1, 4, 1, 48, 64))
+    with pytest.raises(ValueError, match="H, W >= 32"):
+        m(torch.zeros(1, 4, 1, 24, 64))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.zeros(1, 4, 1, 48, 72))
     with pytest.raises(ValueError, match=r"\[B, T, C, H, W\]"):
         m(torch.zeros(4, 1, 64, 64))
     mp = STFLSTMUNet(time_steps=4, use_pk_maps=True)

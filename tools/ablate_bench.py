@@ -26,6 +26,7 @@ def main():
     sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[2:]
     if "slab" in which:
         os.environ["STF_WGRAD_ONE_SLAB"] = "1"
+        os.environ["STF_ABLATION"] = "1"
     import bench
     from stfunet import nhwc, unet
 

@@ -5,6 +5,7 @@ taps' MFMAs and the epilogue), summed over all waves of one launch.
 import os
 import sys
 os.environ["STF_HALO_DIAG"] = "4"
+os.environ["STF_ABLATION"] = "1"
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "stf-unet_amd")]
 import torch
