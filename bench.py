@@ -54,10 +54,6 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
                     help="16-bit activation storage; fp16 = the reference's --amp step (autocast float16 + "
                          "GradScaler, train_and_eval.py:389-404) on the fp16 library")
-    ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
-                    help="replay the training step as a HIP graph (N=1 only; auto = STF).  Off by default: "
-                         "measured slower than eager for STF (12.92 vs 12.49 ms/step), the replay loses most "
-                         "of the LSTM side-stream overlap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timer", action="store_true")
@@ -242,8 +238,11 @@ def cpu_baseline(args):
     same frame size."""
     from oracle import loss as o_loss, optim as o_optim, stf as o_stf, unet as o_unet
     from oracle.init import canonical_state_dict
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
+    # every core this job may use: the CPUs of its affinity mask, unless the host grants the job
+    # a smaller share by OMP_NUM_THREADS (the GPU boxes do: 16 of a shared host's cores per GPU)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    cores = max(1, min(avail, int(omp))) if omp.isdigit() and int(omp) > 0 else avail
     torch.set_num_threads(cores)
     b = 2 if args.size <= 256 else 1           # bounded sample (~10-30 s of CPU work)
     g = torch.Generator().manual_seed(1)
@@ -279,7 +278,8 @@ def cpu_baseline(args):
             f"STFLSTMUNet(T={args.time_steps}{', PK' if args.pk else ''})")
     return {"value": round(b / dt, 4), "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"oracle fp32 {what} train step, batch {b}, {args.size}x{args.size}, "
-                      f"{args.cpu_steps} timed steps after 1 warm-up, {dt:.3f} s/step"}
+                      f"{args.cpu_steps} timed steps after 1 warm-up, {dt:.3f} s/step; {cores} threads "
+                      f"({avail} CPUs in the affinity mask, OMP_NUM_THREADS={omp or 'unset'})"}
 
 
 def _free_port():
@@ -349,13 +349,7 @@ def main():
     fp16 = args.dtype == "fp16"
     model.storage_dtype = torch.float16 if fp16 else torch.bfloat16
     scaler = torch.amp.GradScaler("cuda") if fp16 else None
-    use_graph = args.graph == "on" or (args.graph == "auto" and args.model == "stf" and world == 1)
-    if use_graph and fp16:
-        raise SystemExit("--graph on runs the bf16 step only (GradScaler's inf check syncs the host)")
-    if use_graph and world > 1:
-        raise SystemExit("--graph on needs N=1 (RCCL gradient buckets are not captured)")
-    opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8,
-                capturable=use_graph)
+    opt = AdamW(model.parameters(), lr=1e-3, betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8)
     steps_total = args.warmup + args.steps
     sched = engine.create_lr_scheduler(opt, max(steps_total, 1), 10, warmup=True)
     ddp = GradAllReduce(model) if world > 1 else None
@@ -407,19 +401,10 @@ def main():
     dominant = None
     if not args.no_kernel_timer:
         dominant = max(census, key=lambda k: census[k]["ms"]) if census else None
-    gstep = None
-    if use_graph:
-        from stfunet.graph import TrainStepGraph
-        loss = None                           # drop the last eager step's autograd graph before capture
-        gstep = TrainStepGraph(model, opt, engine.criterion, *batches[0]).capture()
     runtime = model.program.runtime
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if gstep is not None:                 # one replay = the whole step; lr published per step
-            loss = gstep.step(*batches[(args.warmup + i) % len(batches)])
-            sched.step()
-            continue
         if dominant is not None and i == args.steps - 1:
             if runtime.fwd is not None:       # native plan replays: events around that kernel's ranges
                 plan.TIMED = dominant
@@ -431,12 +416,6 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if gstep is not None and dominant is not None:
-        # graph replays cannot be bracketed per launch: time the dominant kernel's launches
-        # in one eager step right after the timed region (same kernels, shapes, buffers)
-        nhwc.TIMER = nhwc.KernelTimer(only=dominant)
-        train_step(args.warmup + args.steps)
-        torch.cuda.synchronize()
     kt = nhwc.TIMER.summary() if nhwc.TIMER is not None else {}
     nhwc.TIMER = None
     if plan.TIMED is not None:
@@ -460,16 +439,13 @@ def main():
             train_gflop = stf_train_flops(args.time_steps, args.size, args.size, args.pk) / 1e9
         workload = workload_name(args)
         roof = roofline(kt, workload, args.batch, census)
-        if gstep is not None and roof:
-            roof["timing"] = "dominant kernel timed in one eager step after the timed graph replays"
         res = {
             "metric": "training samples/sec (256x256 DCE-MRI frames)",
             "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded DCE stacks: noise + wash-in discs), resident in HBM",
-            "execution": ("hip_graph" if gstep is not None else
-                          "native_plan" if runtime.fwd is not None else "eager"),
+            "execution": "native_plan" if runtime.fwd is not None else "eager",
             "config": {"workload": workload,
                        "model": "UNet" if args.model == "unet" else "STFLSTMUNet",
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,

@@ -39,9 +39,9 @@ class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, fused=None,
                  capturable=False, **unused):
         """``capturable=True``: lr and the step count live on the device ({lr, step}
-        per group, ``stf_adamw_dev``), so ``step()`` can be captured in a HIP graph
-        (``stfunet.graph``); call ``graph_sync()`` after the LR scheduler and before
-        each replay to publish the new lr.  Same arithmetic as the host-scalar path."""
+        per group, ``stf_adamw_dev``), so ``step()`` can be captured in a caller's HIP graph
+        (torch's ``capturable`` contract); call ``graph_sync()`` after the LR scheduler and
+        before each replay to publish the new lr.  Same arithmetic as the host-scalar path."""
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self._flat = {}

@@ -97,7 +97,7 @@ def _pool_context(pool):
 
 
 def enabled():
-    # a HIP-graph capture (stfunet/graph.py) records the eager launches itself
+    # inside a caller's HIP-graph capture the eager launches are what gets captured
     return os.environ.get("STF_PLAN", "1") != "0" and not torch.cuda.is_current_stream_capturing()
 
 

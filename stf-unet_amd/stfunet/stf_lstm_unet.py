@@ -291,28 +291,35 @@ class LSTMProgram:
             call("stf_lstm_coop_bwd", _p(st.wcat_t), _p(st.gates), _p(st.c), npix, T, C, dhT.ptr(), dhT.cs,
                  dg.ptr(), d2.ptr(), d2.cs, _p(sync), self.max_wg, self.spin_limit, stream())
             self._note_coop(sync, npix, T)
-        elif st.gates is not None and os.environ.get("STF_LSTM_GATES", "1") != "0":
-            # the cooperative forward kept the activated gates: per step only the cell backward
-            # (elementwise, the same lstm_cell_bwd arithmetic as the recompute epilogue below, so
-            # the same dgates bit for bit) and the [dx | dh] GEMM -- no gate recompute GEMM
-            dc = nhwc.empty((npix, C), torch.float32, dev)
-            for t in range(T - 1, -1, -1):
-                dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
-                dgt = rows(dg, t * B, B)
-                call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None,
-                     dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
-                nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
         else:
+            # BPTT over the per-step launches.  Per step: the cell backward -- from the activated
+            # gates the cooperative forward kept (elementwise stf_lstm_cell_bwd, the arithmetic of
+            # the recompute epilogue, so the same dgates bit for bit), or a recompute of step t's
+            # gates (the forward's GEMM) with the cell backward in its epilogue -- then ONLY the
+            # recurrent half dh_{t-1} = dgates_t W_hh (N = C).  The input half d x_t = dgates_t W_ih
+            # does not feed the recurrence: it is ONE GEMM over all T steps after the loop (SURVEY
+            # section 2.1 K10, src/stf_lstm_unet.py:124-127; STF_LSTM_HOIST=0: [dx | dh] per step).
+            hoist = os.environ.get("STF_LSTM_HOIST", "1") != "0"
+            gates = st.gates is not None and os.environ.get("STF_LSTM_GATES", "1") != "0"
+            w_h = st.wcat_t[4 * C * C:]                     # rows C..2C-1 of [2C][4C]: the h outputs
             dc = nhwc.empty((npix, C), torch.float32, dev)
             for t in range(T - 1, -1, -1):
                 dh = dhT if t == T - 1 else rows(d2, (t + 1) * B, B).slice(C, C)
                 dgt = rows(dg, t * B, B)
-                src = rows(lb, t * B, B)
-                # recompute step t's gates (same GEMM as the forward) + cell backward epilogue
-                epi = LstmEpi(_p(st.c[t - 1]) if t > 0 else None, _p(st.c[t]), None, 0, None,
-                              1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
-                nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
-                nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
+                if gates:
+                    call("stf_lstm_cell_bwd", _p(st.gates[t]), _p(st.c[t]), _p(st.c[t - 1]) if t > 0 else None,
+                         dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr(), npix, C, stream())
+                else:
+                    src = rows(lb, t * B, B)
+                    epi = LstmEpi(_p(st.c[t - 1]) if t > 0 else None, _p(st.c[t]), None, 0, None,
+                                  1, dh.ptr(), dh.cs, _p(dc) if t < T - 1 else None, _p(dc), dgt.ptr())
+                    nhwc.igemm(src, st.wcat, 4 * C, src, 1, 1, 1, 0, bias=st.bias, lstm=epi)
+                if not hoist:
+                    nhwc.igemm(dgt, st.wcat_t, 2 * C, rows(d2, t * B, B), 1, 1, 1, 0)
+                elif t > 0:                                  # dh_{-1} feeds nothing
+                    nhwc.igemm(dgt, w_h, C, rows(d2, t * B, B).slice(C, C), 1, 1, 1, 0)
+            if hoist:
+                nhwc.igemm(dg, st.wcat_t[:4 * C * C], C, d2.slice(0, C), 1, 1, 1, 0)
         dwcat = nhwc.empty(8 * C * C, torch.float32, dev)
         nhwc.wgrad(dg, lb, 1, 1, 1, 0, dwcat, defer=False)
         dbcat = nhwc.empty(4 * C, torch.float32, dev)

@@ -127,13 +127,28 @@ def emulation_dice(tae, bias_shift):
                             num_classes=2)["dice"]
 
 
+class _AutocastBF16(torch.nn.Module):
+    """The reference model with its forward under torch.autocast("cpu", bfloat16), logits
+    returned in fp32: the reference's criterion itself does not run under CPU bf16 autocast
+    (torch.dot of a bf16 softmax and an fp32 one-hot, dice_coefficient_loss.py:32)."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+        self.input_format = getattr(m, "input_format", "time_sequence")
+
+    def forward(self, x):
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            out = self.m(x)
+        return {"out": out["out"].float()}
+
+
 def train_and_eval(stf_mod, tae, threads, autocast_bf16=False):
     torch.set_num_threads(threads)
-    if autocast_bf16:
-        with torch.autocast("cpu", dtype=torch.bfloat16):
-            return train_and_eval(stf_mod, tae, threads)
     model = stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=T)
     model.load_state_dict(canonical_state_dict(model.state_dict(), seed=0))
+    if autocast_bf16:
+        model = _AutocastBF16(model)
     opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3,
                             betas=(0.9, 0.999), weight_decay=1e-4, eps=1e-8, fused=True)
     sched = tae.create_lr_scheduler(opt, STEPS, EPOCHS, warmup=True)
@@ -182,7 +197,7 @@ def main():
         fixed_confmat=fmetrics["confusion_matrix"].mat.numpy(),
         fixed_pred_bits=np.packbits(fpred.reshape(-1)),
         fixed_pred_shape=np.array(fpred.shape),
-        fixed_margin=fmargin,
+        fixed_margin=fmargin.astype(np.float16),
         fixed_bias_shift=np.array(fshift, dtype=np.float32),
         fixed_emu_bf16_ddice=np.array(abs(emu - fmetrics["dice"])),
         fixed_config=np.array([B, T, FIX_HW, FIX_BATCHES]),

@@ -76,10 +76,12 @@ def test_stf_training_from_same_seed_reaches_reference_dice():
     """STF twin (tests/golden/stf_trained.npz, make_golden_trained_stf.py): the reference's own
     train_one_epoch trained STFLSTMUNet(T=4) from the canonical init for 8 x 40 steps of seeded
     [4, 4, 1, 64, 64] DCE stacks (32^2 targets) and its evaluate() scored Dice 0.98091 on 4
-    held-out batches; the same run with 3 instead of 8 CPU threads (reduction order only) scored
-    0.98035 (39 of 16,384 pixels flipped) -- the reference's own run-to-run spread, 5.6e-4.  The
-    gfx950 path (bf16 storage, stfunet AdamW, engine.train_one_epoch / evaluate) trains from the
-    same init on the same batches and must land within 5e-3 (the UNet rule, ~9x that spread)."""
+    held-out batches.  The same reference run differing only in the CPU thread count (reduction
+    order: 3, 1, 5 threads) scored 0.98035 / 0.98071 / 0.97945, and with its model under
+    bf16 autocast (a 16-bit trajectory of the reference itself; 8 and 3 threads) 0.98042 / 0.98022:
+    the reference's own run-to-run band is [0.97945, 0.98091] (1.46e-3 wide).  The gfx950 path
+    (bf16 storage, stfunet AdamW, engine.train_one_epoch / evaluate) trains from the same init on
+    the same batches and must land inside that band widened by 1e-3 on each side (round 3: +-5e-3)."""
     import numpy as np
     import os
     from conftest import GOLDEN
@@ -103,9 +105,11 @@ def test_stf_training_from_same_seed_reaches_reference_dice():
     ev = [dce_case(4000 + i, b, t, hw, hw, target_hw=tgt) for i in range(n_eval)]
     res = engine.evaluate(m, ev, torch.device(DEV), num_classes=2)
     ref = float(z["dice"])
+    band = z["band_dice"].astype(float)
     print(f"STF trained on gfx950: last-epoch loss {loss:.4f} (reference {float(z['train_losses'][-1]):.4f}), "
-          f"dice {res['dice']:.5f} vs reference {ref:.5f} (reference 3-thread rerun {float(z['dice_other_threads']):.5f})")
-    assert abs(res["dice"] - ref) <= 5e-3
+          f"dice {res['dice']:.5f} vs reference {ref:.5f} (reference band {band.min():.5f}..{band.max():.5f} over "
+          f"{', '.join(str(n) for n in z['band_names'])})")
+    assert band.min() - 1e-3 <= res["dice"] <= band.max() + 1e-3
 
 
 def _stf_fixed(z, storage):
@@ -147,8 +151,6 @@ def test_stf_fixed_weight_dice_vs_reference(storage):
     from oracle.cases import dce_case
     from stfunet import engine
     z = np.load(os.path.join(GOLDEN, "stf_trained.npz"))
-    if "fixed_dice" not in z:
-        pytest.skip("TEMP: fixture being regenerated")
     m, (b, t, hw, n) = _stf_fixed(z, storage)
     ev = [dce_case(5000 + i, b, t, hw, hw, target_hw=(hw // 2, hw // 2)) for i in range(n)]
     res = engine.evaluate(m, ev, torch.device(DEV), num_classes=2)

@@ -365,6 +365,7 @@ def test_lstm_whole_sequence_equals_per_step(monkeypatch, T, B, H):
     dhT.buf.normal_()
     prog = LSTMProgram(lstm)
     out = {}
+    monkeypatch.setenv("STF_LSTM_HOIST", "0")            # per-step [dx | dh] like the sequence kernel
     for mode in ("0", "1"):
         monkeypatch.setenv("STF_LSTM_SEQ", mode)
         hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
@@ -398,6 +399,7 @@ def test_lstm_coop_forward_equals_per_step(monkeypatch, C, T, B, H):
     dhT.buf.normal_()
     prog = LSTMProgram(lstm)
     out = {}
+    monkeypatch.setenv("STF_LSTM_HOIST", "0")            # per-step [dx | dh] like the cooperative backward
     for mode in ("0", "1", "g"):
         monkeypatch.setenv("STF_LSTM_COOP", "0" if mode == "0" else "1")
         monkeypatch.setenv("STF_LSTM_COOP_BWD", "1" if mode == "1" else "0")
@@ -685,3 +687,42 @@ def test_stf_size_fallback_vs_oracle():
     print(f"\nSTF 72x104 (size fallback): logits rel {e_hip:.3e} (emu {e_emu:.3e}), loss {loss.item():.6f} vs "
           f"{ref_loss.item():.6f}")
     assert not bad, bad
+
+
+@pytest.mark.parametrize("C,T,B,H", [(64, 5, 3, 6), (128, 8, 16, 32), (256, 8, 16, 16), (512, 8, 16, 8)])
+@pytest.mark.parametrize("gates", [False, True])
+def test_lstm_hoisted_input_projection(monkeypatch, C, T, B, H, gates):
+    """BPTT with the input projection hoisted out of the recurrence (STF_LSTM_HOIST, the default:
+    per step only dh_{t-1} = dgates_t W_hh, then d x for all T steps as ONE GEMM)
+    against the per-step [dx | dh] GEMM: dgates, the weight / bias gradients and d x within rel
+    2e-3 (bitwise where both GEMMs run unsplit: only the split-K choice of the narrower per-step
+    GEMM can change a summation order).  cfg3's lstm2 / lstm3 / lstm4 shapes, both cell-backward
+    sources (gate recompute; the cooperative forward's stored gates)."""
+    from stfunet import nhwc
+    from stfunet.stf_lstm_unet import LSTMProgram
+    monkeypatch.setenv("STF_LSTM_SEQ", "0")
+    monkeypatch.setenv("STF_LSTM_COOP", "1" if gates else "0")
+    monkeypatch.setenv("STF_LSTM_COOP_BWD", "0")
+    if gates and C == 64:
+        pytest.skip("no cooperative forward at C = 64")
+    lstm = torch.nn.LSTM(C, C, batch_first=True).to(DEV)
+    lbuf = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+    lbuf.buf.view(-1, 2 * C)[:, :C].normal_()
+    dhT = nhwc.new_feat(B, H, H, 3 * C, DEV).slice(C, C)
+    dhT.buf.normal_()
+    prog = LSTMProgram(lstm)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("STF_LSTM_HOIST", mode)
+        lb = nhwc.zeros_feat(T * B, H, H, 2 * C, DEV)
+        lb.buf.copy_(lbuf.buf)
+        hT = nhwc.new_feat(B, H, H, 2 * C, DEV).slice(0, C)
+        st = prog.forward(lb, T, B, hT)
+        assert (st.gates is not None) == gates
+        gv = _Grads(lstm)
+        dx = prog.backward(st, dhT, gv)
+        out[mode] = [hT.dense(), dx.dense()] + [gv(p).clone() for p in lstm.parameters()]
+    assert torch.equal(out["0"][0], out["1"][0])             # the forward is untouched
+    for i, (a, b) in enumerate(zip(out["0"][1:], out["1"][1:])):
+        e = ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+        assert e <= 2e-3, (i, e)
