@@ -978,7 +978,15 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // DMA never fills; double-buffered by item parity) and are folded across waves after the next
   // stage-start barrier.
   constexpr bool DEFER = STAGES == 2 && NW == 8 && DIRECT != 0 && !BNR && DIAG == 0;
-  static_assert(!DEFER || (WROWS - 9 * BN) * 64 >= NW * 2 * 64 * 4, "spare weight rows for the statistics");
+  // DEFB (the same kernels with the fused BN-backward reduction): the y tile the reduction needs
+  // is still LDS-DMA'd into the stage just consumed at the end of the item, but nobody waits for
+  // it there: the sums run after the NEXT stage-start barrier, whose vmcnt wait covers the y DMA
+  // (issued before the dz stores), so its latency hides behind the stage transition.  The
+  // partials go to the spare weight rows of that stage and are folded after one more barrier,
+  // before any wave refills the stage.
+  constexpr bool DEFB = STAGES == 2 && NW == 8 && DIRECT == 1 && BNR && DIAG == 0 && IX == 1;
+  static_assert(!(DEFER || DEFB) || (WROWS - 9 * BN) * 64 >= NW * 2 * 64 * 4, "spare weight rows for the statistics");
+  static_assert(!DEFB || NW * 3 * 64 * 4 * 2 + PX * 128 <= (HROWS + 9 * BN) * 64, "y tile below the spare rows");
   static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE && NW * 3 * 64 * 4 * 2 + PX * 128 <= STAGE, "epilogue scratch");
   static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
@@ -1014,7 +1022,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     // DEFER: the lane terms of the DMA addresses are recomputed per fill rather than hoisted
     // out of the stage loop by the compiler (~20 registers the deferred outputs need)
     int sub = lane >> 2, slot = lane & 3;
-    if constexpr (DEFER) asm volatile("" : "+v"(sub), "+v"(slot));
+    if constexpr (DEFER || DEFB) asm volatile("" : "+v"(sub), "+v"(slot));
     const int nt = item / ntiles, tile = item - nt * ntiles;
     const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
@@ -1039,7 +1047,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       if (HI + i < k0 || HI + i >= k1 || !wload) continue;
-      if (DEFER && (wave * WI + i) * RPI >= 9 * BN) continue;   // wholly past the rows: keep the spare rows
+      if ((DEFER || DEFB) && (wave * WI + i) * RPI >= 9 * BN) continue;   // wholly past the rows: keep the spare rows
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
@@ -1159,6 +1167,65 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       s12d[h] = row16_reduce_scatter(v, fr);
     }
   };
+  // DEFB state: bpend = an item's packed dz (uq, mq) and its y tile (LDS stage bbuf) wait for the
+  // next stage-start barrier; its BN affine (scale, shift, mean, invstd) of this lane's channel
+  bool bpend = false;
+  int bbuf = 0, bkey = 0, bitem = 0;
+  auto bnr_finish = [&]() {
+    {                                                    // the pixel rows again (4 registers fewer live)
+      const int nt = bitem / ntiles, tile = bitem - nt * ntiles;
+      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) mq[i] = halo_pixel<PH, PW, IX>(wave * WTM + i * 16 + fr, tq * IX, ty, tx, a.Hd, a.Wd);
+    }
+    // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat) per channel, as the in-item epilogue below
+    char* sb = smem + bbuf * STAGE;
+    const float* aff = reinterpret_cast<const float*>(sb + NW * 2 * 64 * 4) + wave * 256;
+    const char* yl = sb + NW * 3 * 64 * 4 * 2 + wave * WTM * 128;
+    float* red = red_d(bbuf);
+    auto aff8 = [&](int k, int c0, float* v) {
+      const float4 lo = *reinterpret_cast<const float4*>(aff + k * 64 + c0);
+      const float4 hi = *reinterpret_cast<const float4*>(aff + k * 64 + c0 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    };
+    const bool norelu = !a.bnr_relu;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float q1[8], q2[8], sc[8], sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { q1[e] = 0.f; q2[e] = 0.f; }
+      aff8(0, h * 32 + fk * 8, sc);
+      aff8(1, h * 32 + fk * 8, sh);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float g[8], yv[8];
+        unpack8(uq[h][i], g);
+        const int r = i * 16 + fr;
+        unpack8(*reinterpret_cast<const uint4*>(yl + r * 128 + (((h * 4 + fk) ^ (r & 7)) << 4)), yv);
+        const bool valid = mq[i] >= 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool keep = valid & (norelu | (yv[e] * sc[e] + sh[e] > 0.f));
+          const float gg = keep ? g[e] : 0.f;
+          q1[e] += gg;
+          q2[e] += gg * yv[e];
+        }
+      }
+      float mu[8], is[8], v[16];
+      aff8(2, h * 32 + fk * 8, mu);
+      aff8(3, h * 32 + fk * 8, is);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = q1[e];
+        v[8 + e] = is[e] * (q2[e] - mu[e] * q1[e]);
+      }
+      red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = row16_reduce_scatter(v, fr);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                        // every wave's partials are in, its y reads done
+    fold_stats(red, bkey);
+    bpend = false;
+  };
   auto put_sums = [&](int rb) {
     float* red = red_d(rb);
 #pragma unroll
@@ -1212,6 +1279,9 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
           fold_stats(red_d(fold_rb), fold_key);
           fold = false;
         }
+      }
+      if constexpr (DEFB) {
+        if (bpend) bnr_finish();                         // the vmcnt wait above covered the y DMA
       }
       load_bias();
       const bool live = s + 1 < S;
@@ -1367,9 +1437,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
       const __amdgpu_buffer_rsrc_t rs_dst =
           __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      uint4 uq[2][TM];
-      int mq[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int p = wave * WTM + i * 16 + fr;
@@ -1427,6 +1494,18 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
               mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
         }
+      if constexpr (DEFB) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) aff[k * 64 + lane] = aff_pre[k];   // read back by this wave only
+        bpend = true;
+        bbuf = buf;
+        bkey = (img / ipg) * NTn + nt;
+        bitem = cit;
+        ccc = 0;
+        ++cit;
+        epi = true;
+        continue;
+      }
       if constexpr (BNR) {
         // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat), like stf_bn_bwd_reduce
 #pragma unroll
@@ -1617,6 +1696,13 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       ccc = 0;
       ++cit;
       epi = true;
+    }
+  }
+  if constexpr (DEFB) {
+    if (bpend) {                                         // the last item's y tile and reduction
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+      __builtin_amdgcn_s_barrier();
+      bnr_finish();
     }
   }
   if constexpr (DEFER) {

@@ -225,23 +225,37 @@ steps(a)                                     # a's plans and private pool are re
 c = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
 steps(c)
 assert pools(a) == 1 and pools(c) == 1, (pools(a), pools(c))
+import weakref
 a.cycle = a                                  # only the cyclic collector can free a (and its pool) now
+a_prog, a_rt = weakref.ref(a.program), weakref.ref(a.program.runtime)
+try:
+    a_pool = weakref.ref(next(iter(a.program.runtime.entries.values())).pool)
+except TypeError:                            # a pool type without weak references: not checked
+    a_pool = lambda: False
 del a
 seen = []
 def hook(rt, phase):                         # inside b's recording, its pool context open
     if seen:
         return
     c.program.runtime.close()                # drop the last reference to another live entry's pool
+    after_close = len(plan._GRAVEYARD)
     n = gc.collect()                         # collect the dead program a, its entry and pool
-    seen.append((phase, n, len(plan._GRAVEYARD), plan._POOL_ACTIVE))
+    seen.append((phase, n, after_close, len(plan._GRAVEYARD), plan._POOL_ACTIVE,
+                 a_prog() is None, a_rt() is None, a_pool() is None))
 plan.RECORD_HOOK = hook
 b = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
 steps(b)                                     # b records: the hook runs inside the recording
 plan.RECORD_HOOK = None
-phase, n, buried, active = seen[0]
-assert phase == "forward" and n > 0 and active == 1, seen
-assert buried == 2, seen                     # a's and c's pools: deferred, not destroyed in the context
+print(seen)
+phase, n, after_close, buried, active, prog_dead, rt_dead, pool_dead = seen[0]
+assert phase == "forward" and active == 1, seen
+assert after_close >= 1, seen                # c's pool: deferred, not destroyed inside the context
+assert not pool_dead, seen                   # nothing destroyed a pool inside the context
+assert prog_dead and rt_dead, seen           # the dead program was collected (its pool buried)
+assert buried >= after_close + 1, seen
 assert not plan._GRAVEYARD, len(plan._GRAVEYARD)   # destroyed at the recording's exit
+gc.collect()
+assert a_pool() in (None, False)             # ... and gone
 steps(c)                                     # c records again from scratch
 torch.cuda.synchronize()
 print("ok")
@@ -255,8 +269,8 @@ def test_plan_pool_lifetime_is_explicit():
     process, the GC-off guard bypassed): inside program b's forward recording a hook closes
     program c's runtime -- dropping the last reference to its pool -- and runs gc.collect()
     over a dead program a held only by a reference cycle.  Both pools must go to the graveyard
-    (2 entries, pool context count 1 at that moment) and be destroyed when the recording's
-    context exits; the process exits cleanly and c records again afterwards."""
+    (pool context count 1 at that moment, neither pool destroyed) and be destroyed once the
+    recording's context exits; the process exits cleanly and c records again afterwards."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

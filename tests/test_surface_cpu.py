@@ -74,6 +74,17 @@ def test_library_rejects_bad_shapes_without_launch():
     assert lib.stf_igemm(ctypes.byref(a), None) == 100001
     assert lib.stf_bn_act(None, 8, 1, 4, 4, 12, 1, None, None, 1, None, 0, None, None, None, 12, None,
                           None) == 100001
+    # stem BN+ReLU+MaxPool(3,2,1) (stf.hip bn_act_maxpool3): its unit index is 32-bit,
+    # so a launch whose N*Ho*Wo*C/8 units (plus the grid stride) reach 2^31 is refused up front;
+    # the largest accepted one writes through 64-bit offsets.  Fake non-null pointers: nothing runs.
+    fake = ctypes.c_void_p(1 << 20)
+    big = (1 << 31) // (128 * 128 * 8) + 1              # 512^2 input, C = 64: 128 x 128 x 8 units per image
+    assert lib.stf_bn_act_maxpool3s2(fake, big, 256, 256, 64, 1, fake, fake, fake, fake, None) == 100001
+    assert lib.stf_bn_act_maxpool3s2(fake, 8, 256, 256, 12, 1, fake, fake, fake, fake, None) == 100001
+    # the DecoderBlock size fallback's argument checks (C % 8, strides, alignment)
+    assert lib.stf_bilinear_ac_fwd(fake, 1, 6, 8, 12, 12, fake, 5, 7, 12, None) == 100001
+    assert lib.stf_bilinear_ac_bwd(fake, 1, 5, 7, 64, 60, fake, 6, 8, 64, None) == 100001
+    assert lib.stf_bilinear_ac_fwd(ctypes.c_void_p(8), 1, 6, 8, 64, 64, fake, 5, 7, 64, None) == 100001
 
 
 def test_preprocess_and_lr_schedule_match_reference():
