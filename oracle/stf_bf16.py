@@ -89,6 +89,8 @@ def forward(p, x, training=True, use_pk_maps=False, pk_channels=3):
     for name, skip in (("decoder4", e3), ("decoder3", e2), ("decoder2", e1)):
         up = q(F.conv_transpose2d(d, q(p[f"{name}.up.weight"], False), p[f"{name}.up.bias"], stride=2, padding=1,
                                   output_padding=1))
+        if up.shape[2:] != skip.shape[2:]:          # the size fallback (src/stf_lstm_unet.py:56-57)
+            up = q(F.interpolate(up, size=skip.shape[2:], mode="bilinear", align_corners=True))
         hcat = _conv(torch.cat([up, skip], 1), p[f"{name}.fusion.weight"], p[f"{name}.fusion.bias"])
         d = _rcb(hcat, p, f"{name}.res_conv", training)
     d = q(F.conv_transpose2d(d, q(p["upconv1.weight"], False), p["upconv1.bias"], stride=2, padding=1,

@@ -38,10 +38,11 @@ class KernelTimer:
     accumulates algorithmic FLOPs per device kernel (bench.py's roofline).
     ``only``: instrument just this kernel name (the others cost nothing)."""
 
-    def __init__(self, only=None):
+    def __init__(self, only=None, log=False):
         self.rec = {}
         self.only = only
         self.tags = {}       # tag -> {"conv": [(ev0, ev1, flops)], "block": [(ev0, ev1)]}
+        self.log = [] if log else None     # per launch: (shape, kernel, ev0, ev1, stream) in issue order
 
     def wants(self, name):
         return self.only is None or name == self.only
@@ -83,10 +84,12 @@ class KernelTimer:
         ev.record(torch.cuda.current_stream())
         return ev
 
-    def end(self, ev0, family, flops):
+    def end(self, ev0, family, flops, desc=None):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record(torch.cuda.current_stream())
         self.rec.setdefault(family, []).append((ev0, ev1, flops))
+        if self.log is not None:
+            self.log.append((desc, family, ev0, ev1, torch.cuda.current_stream().stream_id, flops))
         if TIMER_TAG is not None:
             self.tags.setdefault(TIMER_TAG, {"conv": [], "block": []})["conv"].append((ev0, ev1, flops))
 
@@ -407,7 +410,9 @@ def igemm(src: Feat, wgt, nout, dst: Feat, R, S, stride, pad, transposed=False, 
         call("stf_plan_tag_end")
     if t is not None:
         macs = src.N * Hd * Wd * nout * R * S * src.C
-        t.end(ev, name, 2.0 * macs / (stride * stride if transposed else 1))
+        t.end(ev, name, 2.0 * macs / (stride * stride if transposed else 1),
+              f"igemm M={src.N * Hd * Wd} N={nout} K={R * S * src.C} {R}x{S}/s{stride}{' T' if transposed else ''}"
+              f"{' lstm' if lstm is not None else ''}{' bnr' if bnr is not None else ''}")
     return stats, tiles
 
 
@@ -524,7 +529,8 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
     if RECORDING:
         call("stf_plan_tag_end")
     if t is not None:
-        t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C)
+        t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C,
+              f"wgrad M={dy.M} N={dy.C} K={R * S * x.C} {R}x{S}/s{stride} splits={splits}")
     call("stf_wgrad_reduce", ws.data_ptr(), splits, dy.C, R, S, x.C, out.data_ptr(), stream())
 
 

@@ -257,14 +257,36 @@ def gen_keys(unet_mod, stf_mod, out):
         json.dump(res, f)
 
 
+def gen_stf_size_fallback(stf_mod, tae, out):
+    """STFLSTMUNet(T=3) at 72 x 104 (not divisible by 32): the reference's DecoderBlock resizes the
+    transposed-conv outputs of decoder4 / decoder3 to the skips by bilinear interpolation
+    (src/stf_lstm_unet.py:56-57).  Train-mode logits, loss and gradient checksums."""
+    model = stf_mod.STFLSTMUNet(in_channels=1, num_classes=2, time_steps=3)
+    model.load_state_dict(canonical_state_dict(model.state_dict(), seed=0))
+    x, tgt = dce_case(7, 1, 3, 72, 104, target_hw=(36, 52))
+    model.train()
+    outd = model(x)
+    loss = tae.criterion(outd, tgt)
+    loss.backward()
+    res = {"x": x.numpy(), "target": tgt.numpy(), "logits": outd["out"].detach().numpy(),
+           "loss": np.array(loss.item())}
+    for k, p in model.named_parameters():
+        res["gradck." + k] = _cksum(p.grad)
+    np.savez_compressed(os.path.join(out, "stf_t3_72x104.npz"), **res)
+    return {"stf_t3_72x104.npz": loss.item()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
-    ap.add_argument("--only", default=None, choices=["keys"], help="regenerate one fixture only")
+    ap.add_argument("--only", default=None, choices=["keys", "fallback"], help="regenerate one fixture only")
     a = ap.parse_args()
     torch.set_num_threads(8)
     unet_mod, stf_mod, tae, dcl = load_reference(a.ref)
+    if a.only == "fallback":
+        print(gen_stf_size_fallback(stf_mod, tae, a.out))
+        return
     gen_keys(unet_mod, stf_mod, a.out)
     if a.only == "keys":
         return
@@ -273,6 +295,7 @@ def main():
     summary.update(gen_unet_full(unet_mod, tae, a.out))
     summary.update(gen_stf(stf_mod, tae, a.out, pk=False))
     summary.update(gen_stf(stf_mod, tae, a.out, pk=True))
+    summary.update(gen_stf_size_fallback(stf_mod, tae, a.out))
     gen_criterion(tae, dcl, a.out)
     gen_metrics(tae, a.out)
     gen_lr(tae, a.out)

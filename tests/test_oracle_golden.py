@@ -200,3 +200,30 @@ def test_trained_unet_dice_oracle_vs_reference():
     assert np.array_equal(np.concatenate(preds), tr["pred"])
     assert abs(float(np.mean(dices, axis=0).mean()) - tr["dice"]) < 1e-6
     assert tr["dice"] > 0.98
+
+
+def test_stf_size_fallback_matches_reference():
+    """The restatement's DecoderBlock size fallback (bilinear, align_corners=True, on a size
+    mismatch; src/stf_lstm_unet.py:56-57) against the reference run at 72 x 104 (make_golden.py
+    gen_stf_size_fallback): train-mode logits, loss and every parameter gradient's checksum, in
+    fp32 and through the bf16-storage emulation's structure (shapes)."""
+    import oracle.unet_bf16 as o_q
+    from oracle import stf_bf16 as o_emu
+    g = _g("stf_t3_72x104.npz")
+    tpl = o_stf.template_state_dict()                       # (no T in the parameter shapes)
+    p = _params(canonical_state_dict(tpl, seed=0))
+    x = torch.from_numpy(g["x"])
+    out = o_stf.forward(p, x, training=True)["out"]
+    loss = o_loss.criterion(out, torch.from_numpy(g["target"]))
+    loss.backward()
+    assert out.shape == g["logits"].shape == (1, 2, 36, 52)
+    assert _rel(out.detach(), g["logits"]) < 1e-4
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    grads = _grads(p)
+    for k in g.files:
+        if k.startswith("gradck."):
+            got = grads[k[7:]].double()
+            assert abs(got.abs().sum().item() - g[k][1]) <= 2e-3 * abs(g[k][1]) + 1e-6 * got.numel(), k
+    with torch.no_grad(), o_q.storage(torch.bfloat16):
+        emu = o_emu.forward({k: v.detach() for k, v in p.items()}, x, True)["out"]
+    assert emu.shape == out.shape and _rel(emu, g["logits"]) < 0.3

@@ -626,17 +626,17 @@ def test_bilinear_align_corners_kernels(H, W, h, w):
     x.buf.normal_()
     y = nhwc.new_feat(N, h, w, 2 * C, DEV).slice(0, C)
     _lib.call("stf_bilinear_ac_fwd", x.ptr(), N, H, W, C, x.cs, y.ptr(), h, w, y.cs, _lib.stream())
-    xr = x.dense().float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    xr = x.dense().contiguous().requires_grad_(True)                  # dense(): [N, C, H, W] fp32
     ref = F.interpolate(xr, size=(h, w), mode="bilinear", align_corners=True)
-    got = y.dense().float().permute(0, 3, 1, 2)
+    got = y.dense()
     assert rel(got, ref) <= 1e-2, rel(got, ref)
     assert (got - ref.to(torch.bfloat16).float()).abs().max().item() <= 2e-2 * ref.abs().max().item()
     dy = nhwc.new_feat(N, h, w, C + 16, DEV).slice(16, C)
     dy.buf.normal_()
     dx = nhwc.new_feat(N, H, W, C, DEV)
     _lib.call("stf_bilinear_ac_bwd", dy.ptr(), N, h, w, C, dy.cs, dx.ptr(), H, W, dx.cs, _lib.stream())
-    ref.backward(dy.dense().float().permute(0, 3, 1, 2))
-    gdx = dx.dense().float().permute(0, 3, 1, 2)
+    ref.backward(dy.dense())
+    gdx = dx.dense()
     assert rel(gdx, xr.grad) <= 1e-2, rel(gdx, xr.grad)
 
 
