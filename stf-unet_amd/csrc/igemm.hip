@@ -13,7 +13,6 @@
 // are 64 B; the 16-B chunk of row r is stored at chunk ^ ((-(r>>2)) & 3), which
 // makes the ds_read_b128 fragment reads conflict-free for all four lane groups.
 #include "common.h"
-#include <type_traits>
 #include "../../include/stfunet.h"
 #include <stdio.h>
 #include <stdlib.h>
@@ -968,24 +967,18 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // instructions over the taps only moves the stall into the taps: the DMA path itself
   // is the limit, fewer bytes per FLOP is what would help.
   constexpr bool STAGGER = STAGES == 2 && NW == 8;
-  // DEFER (2-stage direct epilogues without the fused BN-backward reduction): the end of an
-  // item is no longer a phase of its own with two barriers, where every wave of the CU stalls on
-  // the store path at once with the MFMA pipes idle.  The accumulators are packed to 16 bits,
-  // the first half of the output stores (channels 0-31) goes out at once and the second half
-  // (16 registers) between the taps of the next stage (even waves at taps 0.., behind their
-  // stage-start DMA, odd waves at taps 4.., behind the DMA they issue there: vmcnt stays exact).
-  // The BN statistics' partials go to spare weight rows (rows 9*64.. of a stage, which the weight
-  // DMA never fills; double-buffered by item parity) and are folded across waves after the next
-  // stage-start barrier.
-  constexpr bool DEFER = STAGES == 2 && NW == 8 && DIRECT != 0 && !BNR && DIAG == 0;
-  // DEFB (the same kernels with the fused BN-backward reduction): the y tile the reduction needs
-  // is still LDS-DMA'd into the stage just consumed at the end of the item, but nobody waits for
-  // it there: the sums run after the NEXT stage-start barrier, whose vmcnt wait covers the y DMA
-  // (issued before the dz stores), so its latency hides behind the stage transition.  The
-  // partials go to the spare weight rows of that stage and are folded after one more barrier,
-  // before any wave refills the stage.
+  // DEFB (2-stage kernels with the fused BN-backward reduction, single-image tiles): the y tile
+  // the reduction needs is still LDS-DMA'd into the stage just consumed at the end of the item,
+  // but nobody waits for it there: the sums run after the NEXT stage-start barrier, whose vmcnt
+  // wait covers the y DMA (issued before the dz stores), so its latency hides behind the stage
+  // transition.  The partials go to spare weight rows of that stage (rows 9*64.. of a stage,
+  // which the weight DMA never fills) and are folded after one more barrier, before any wave
+  // refills the stage.  (Same-box A/B, profiles/r04/ab_halo_epilogue.txt: the halo dgrads -1 %;
+  // deferring the output stores of the other direct epilogues into the next stage's taps instead
+  // cost +5 % -- they compete with the stage's DMA for the vector-memory address path -- and a
+  // barrier-free statistics fold was neutral: neither is built.)
   constexpr bool DEFB = STAGES == 2 && NW == 8 && DIRECT == 1 && BNR && DIAG == 0 && IX == 1;
-  static_assert(!(DEFER || DEFB) || (WROWS - 9 * BN) * 64 >= NW * 2 * 64 * 4, "spare weight rows for the statistics");
+  static_assert(!DEFB || (WROWS - 9 * BN) * 64 >= NW * 2 * 64 * 4, "spare weight rows for the partials");
   static_assert(!DEFB || NW * 3 * 64 * 4 * 2 + PX * 128 <= (HROWS + 9 * BN) * 64, "y tile below the spare rows");
   static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE && NW * 3 * 64 * 4 * 2 + PX * 128 <= STAGE, "epilogue scratch");
@@ -1019,10 +1012,10 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // of the stage only streams the halo (half the DMA instructions at 64 source channels).
   int wkey0 = -1, wkey1 = -1;
   auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1, bool wload) {
-    // DEFER: the lane terms of the DMA addresses are recomputed per fill rather than hoisted
-    // out of the stage loop by the compiler (~20 registers the deferred outputs need)
+    // DEFB: the lane terms of the DMA addresses are recomputed per fill rather than hoisted out
+    // of the stage loop by the compiler (the registers the deferred reduction keeps live)
     int sub = lane >> 2, slot = lane & 3;
-    if constexpr (DEFER || DEFB) asm volatile("" : "+v"(sub), "+v"(slot));
+    if constexpr (DEFB) asm volatile("" : "+v"(sub), "+v"(slot));
     const int nt = item / ntiles, tile = item - nt * ntiles;
     const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
@@ -1047,7 +1040,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       if (HI + i < k0 || HI + i >= k1 || !wload) continue;
-      if ((DEFER || DEFB) && (wave * WI + i) * RPI >= 9 * BN) continue;   // wholly past the rows: keep the spare rows
+      if (DEFB && (wave * WI + i) * RPI >= 9 * BN) continue;   // wholly past the rows: keep the spare rows
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
@@ -1115,17 +1108,9 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
   bool wl_next = true;                                   // the next fill streams weight rows too
-  // DEFER state: pend = the last packed item's second store half waits in uq[1] / mq (slice pnt)
-  // for the next stage's taps; fold = an item's statistics partials wait in red_d(fold_rb) (key
-  // fold_key) for the next stage-start barrier; nst = stores issued behind this stage's DMA
-  bool pend = false, fold = false;
-  int nst = 0, ipar = 0, fold_rb = 0, fold_key = 0;
-  uint4 uq[2][TM];
-  int mq[TM];
-  float s12d[2] = {0.f, 0.f};
+  uint4 uq[2][TM];                                       // direct epilogue: the packed outputs
+  int mq[TM];                                            // ... and their pixel rows (-1: outside)
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const __amdgpu_buffer_rsrc_t rs_out =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, (uint32_t)((size_t)a.M * a.dcs * 2), 0x00020000);
   auto red_d = [&](int rb) { return reinterpret_cast<float*>(smem + rb * STAGE + (HROWS + 9 * BN) * 64); };
   auto fold_stats = [&](const float* red, int key) {
     if (tid < 128) {
@@ -1139,32 +1124,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
         run = 0.f;
       }
       run += t;
-    }
-  };
-  uint32_t soff[TM];                                     // byte offsets of the first half's stores
-  auto store_out = [&](int k) {                          // output store k (half k / TM) of the packed item
-    const int h = k / TM, i = k - h * TM;
-    const uint4 u = uq[h][i];
-    // the second half sits 64 B after the first (channels 32..63); an invalid pixel's offset
-    // is past the buffer either way
-    const uint32_t off = h ? (soff[i] == 0xFFFFFFF0u ? soff[i] : soff[i] + 64u) : soff[i];
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_out, off, 0, 0);
-  };
-  auto pend_sums = [&]() {                               // BN statistics of the pending item's stored values
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float g[8];
-        unpack8(uq[h][i], g);
-        const float w = mq[i] >= 0 ? 1.f : 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { v[e] += w * g[e]; v[8 + e] += w * g[e] * g[e]; }
-      }
-      s12d[h] = row16_reduce_scatter(v, fr);
     }
   };
   // DEFB state: bpend = an item's packed dz (uq, mq) and its y tile (LDS stage bbuf) wait for the
@@ -1226,11 +1185,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     fold_stats(red, bkey);
     bpend = false;
   };
-  auto put_sums = [&](int rb) {
-    float* red = red_d(rb);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = s12d[h];
-  };
+
   // DIAG 4: per-wave cycle buckets (s_memtime) -- DMA wait, barrier, DMA issue, taps, epilogue
   uint64_t tb[5] = {0, 0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
@@ -1261,25 +1216,12 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     if constexpr (STAGES == 2) {
       // retire this stage's DMA; the previous epilogue's NSTORE buffer stores
       // (issued after it, stores and loads retire in order) may stay in flight
-      if constexpr (DEFER) {
-        if (nst == NSTORE) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
-        else if (nst) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE / 2) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        nst = 0;
-      } else {
-        if (epi) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (epi) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(0);
       epi = false;
       __builtin_amdgcn_s_barrier();
       stamp(1);
-      if constexpr (DEFER && DIRECT == 2) {
-        if (fold) {                                      // every wave's partials of the item are in
-          fold_stats(red_d(fold_rb), fold_key);
-          fold = false;
-        }
-      }
       if constexpr (DEFB) {
         if (bpend) bnr_finish();                         // the vmcnt wait above covered the y DMA
       }
@@ -1324,23 +1266,12 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
         asm volatile("ds_read_b128 %0, %1 offset:%2"
                      : "=v"(wf[b][j]) : "v"(hb32 + wrow0), "i"((t * BN + j * 16) * 64));
     };
-    // PEND: this stage also issues the pending item's second store half (TM stores: even waves
-    // from tap 0, after their stage-start DMA; odd waves from tap 4, after the DMA they issue
-    // there).
-    auto taps = [&](auto pend_c, auto odd_c) {
-    constexpr bool PEND = decltype(pend_c)::value, ODD = decltype(odd_c)::value;
     rd_tap(0, 0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int b = t & 1;
       if constexpr (STAGGER) {
-        if (t == 4 && (wave & 1) != 0)
-          issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
-      }
-      if constexpr (DEFER) {                          // the pending second half: one store per tap
-        // (one tap loop for both cases -- two copies of it cost ~40 registers more: spills)
-        const int T0 = (wave & 1) ? 4 : 0;
-        if (pend && t >= T0 && t < T0 + TM) store_out(TM + t - T0);
+        if (t == 4 && (wave & 1)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
       }
       if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
       // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
@@ -1366,63 +1297,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
         for (int j = 0; j < TN; ++j)
           acc[i][j] = mfma16x16x32(wf[b][j], xf[b][i], acc[i][j]);
     }
-    };
-    using c_true = std::integral_constant<bool, true>;
-    using c_false = std::integral_constant<bool, false>;
-    if constexpr (DEFER) {
-      taps(c_true{}, c_false{});
-      nst = pend ? NSTORE / 2 : 0;
-      pend = false;
-    } else {
-      taps(c_false{}, c_false{});
-    }
     stamp(3);
-    if (DEFER && ccc + 1 == CC) {
-      // ---- deferred direct epilogue: pack only (the next stage stores and sums)
-      const int nt = cit / ntiles, tile = cit - nt * ntiles;
-      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int p = wave * WTM + i * 16 + fr;
-        mq[i] = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float f[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            f[r] = acc[i][2 * h][r] + bv[2 * h][r];
-            f[4 + r] = acc[i][2 * h + 1][r] + bv[2 * h + 1][r];
-          }
-          if (a.accumulate && mq[i] >= 0) {
-            float o[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8), o);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] += o[e];
-          }
-          uq[h][i] = pack8(f);
-          acc[i][2 * h] = f32x4{0.f, 0.f, 0.f, 0.f};
-          acc[i][2 * h + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        soff[i] = mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + fk * 8) * 2) : 0xFFFFFFF0u;
-#pragma unroll
-      for (int k = 0; k < TM; ++k) store_out(k);         // the first half now
-      nst += NSTORE / 2;
-      if constexpr (DIRECT == 2) {                       // partials for the next stage-start fold
-        pend_sums();
-        put_sums(ipar);
-        fold = true;
-        fold_rb = ipar;
-        fold_key = (img / ipg) * NTn + nt;
-        ipar ^= 1;
-      }
-      pend = true;
-      ccc = 0;
-      ++cit;
-      continue;
-    }
     if (DIRECT && ccc + 1 == CC) {
       // ---- direct epilogue: lane (fr, fk) holds pixel p's channels 8fk..8fk+7 (fragments
       // 0,1) and 32+8fk.. (2,3).  Order: pack the accumulators (64 fp32 -> 32 bf16x2
@@ -1703,20 +1578,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
       __builtin_amdgcn_s_barrier();
       bnr_finish();
-    }
-  }
-  if constexpr (DEFER) {
-    // the last item's second store half and statistics fold
-    if (pend) {
-#pragma unroll
-      for (int k = 0; k < TM; ++k) store_out(TM + k);
-    }
-    if constexpr (DIRECT == 2) {
-      if (fold) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        fold_stats(red_d(fold_rb), fold_key);
-      }
     }
   }
   if (sbuf && tid < 128 && run_key >= 0) flush();

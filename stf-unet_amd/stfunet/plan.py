@@ -59,10 +59,14 @@ _POOL_ACTIVE = 0       # recording pool contexts open in this process (any threa
 _GRAVEYARD = []        # released pools, destroyed by drain_pools() at a safe point
 
 
+POOL_EVENTS = {"buried": 0, "destroyed": 0, "entry_del": 0}   # counters (tests)
+
+
 def _bury(pool):
     if pool is not None:
         with _POOL_LOCK:
             _GRAVEYARD.append(pool)
+            POOL_EVENTS["buried"] += 1
 
 
 def drain_pools():
@@ -75,6 +79,7 @@ def drain_pools():
             return
         dead = _GRAVEYARD[:]
         _GRAVEYARD.clear()
+        POOL_EVENTS["destroyed"] += len(dead)
         dead.clear()
 
 
@@ -191,6 +196,7 @@ class _Entry:
     def __del__(self):
         # by refcount or inside a cyclic collection, possibly while another recording's pool
         # context is open: never destroy the pool here
+        POOL_EVENTS["entry_del"] += 1
         pool = getattr(self, "pool", None)
         if pool is not None:
             self.pool = None

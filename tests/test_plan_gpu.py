@@ -228,12 +228,10 @@ assert pools(a) == 1 and pools(c) == 1, (pools(a), pools(c))
 import weakref
 a.cycle = a                                  # only the cyclic collector can free a (and its pool) now
 a_prog, a_rt = weakref.ref(a.program), weakref.ref(a.program.runtime)
-try:
-    a_pool = weakref.ref(next(iter(a.program.runtime.entries.values())).pool)
-except TypeError:                            # a pool type without weak references: not checked
-    a_pool = lambda: False
+a_pool = lambda: None                        # (weak references to a collected pool clear even if rescued)
 del a
 seen = []
+ev0 = dict(plan.POOL_EVENTS)
 def hook(rt, phase):                         # inside b's recording, its pool context open
     if seen:
         return
@@ -241,21 +239,20 @@ def hook(rt, phase):                         # inside b's recording, its pool co
     after_close = len(plan._GRAVEYARD)
     n = gc.collect()                         # collect the dead program a, its entry and pool
     seen.append((phase, n, after_close, len(plan._GRAVEYARD), plan._POOL_ACTIVE,
-                 a_prog() is None, a_rt() is None, a_pool() is None))
+                 a_prog() is None, a_rt() is None, a_pool() is None, dict(plan.POOL_EVENTS)))
 plan.RECORD_HOOK = hook
 b = UNet(in_channels=8, num_classes=2, base_c=8).cuda().train()
 steps(b)                                     # b records: the hook runs inside the recording
 plan.RECORD_HOOK = None
-print(seen)
-phase, n, after_close, buried, active, prog_dead, rt_dead, pool_dead = seen[0]
+print(seen, plan.POOL_EVENTS)
+phase, n, after_close, buried, active, prog_dead, rt_dead, pool_dead, ev = seen[0]
 assert phase == "forward" and active == 1, seen
 assert after_close >= 1, seen                # c's pool: deferred, not destroyed inside the context
-assert not pool_dead, seen                   # nothing destroyed a pool inside the context
-assert prog_dead and rt_dead, seen           # the dead program was collected (its pool buried)
-assert buried >= after_close + 1, seen
+assert prog_dead and rt_dead, seen           # the dead program was collected ...
+assert ev["entry_del"] >= 1 and buried >= after_close + 1, seen   # ... its entry's pool buried, not freed
+assert ev["destroyed"] == ev0["destroyed"], (seen, ev0)           # nothing destroyed inside the context
 assert not plan._GRAVEYARD, len(plan._GRAVEYARD)   # destroyed at the recording's exit
-gc.collect()
-assert a_pool() in (None, False)             # ... and gone
+assert plan.POOL_EVENTS["destroyed"] >= ev0["destroyed"] + 2, (plan.POOL_EVENTS, ev0)
 steps(c)                                     # c records again from scratch
 torch.cuda.synchronize()
 print("ok")
