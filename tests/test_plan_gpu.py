@@ -213,6 +213,7 @@ sys.path.insert(0, "stf-unet_amd")
 from stfunet import UNet, engine, plan
 from stfunet.synthetic import dce_batch
 plan._no_gc = contextlib.nullcontext          # the GC-off guard bypassed: the pool lifetime alone
+gc.disable()                                 # collections only where this script asks for them
 x, t = dce_batch(2, 8, 64, 64, seed=0, device="cuda")
 x = x.flatten(1, 2)
 def steps(m):

@@ -8,10 +8,11 @@
 #   4. the PK-map fit bench (tools/bench_pk.py) under rocprofv3, the eval-metric micro-bench
 # Outputs (summaries only) under gpurun_out/prof_<tag>; copy into profiles/<tag>.
 set -e
-tag=${1:-r03}
+tag=${1:-r04}
 root=$GRAFT_REPO_ROOT
 out=$root/gpurun_out/prof_$tag
 mkdir -p $out
+if [ -z "$ONLY_PMC" ]; then
 timeout -k 10 600 python3 bench.py > $out/bench_unet256_b64.json 2> $out/bench_unet.err
 timeout -k 10 600 python3 bench.py --model stf > $out/bench_stf256_t8_b16.json 2> $out/bench_stf.err
 timeout -k 10 600 python3 bench.py --config 4 --steps 20 --warmup 5 > $out/bench_cfg4_stf256_t16_b16.json 2> $out/bench_cfg4.err
@@ -31,6 +32,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/a
 cd $root
 timeout -k 10 200 python3 tools/bench_eval.py > $out/bench_eval.txt 2>&1
 timeout -k 10 200 python3 tools/bench_aug.py > $out/bench_aug.json 2> $out/bench_aug.err
+cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
+cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
+cp $out/cfg5/run_kernel_stats.csv $out/cfg5_stf512_t32pk_b4_fp16_kernel_stats.csv
+cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
+cp $out/aug/run_kernel_stats.csv $out/aug_b16_kernel_stats.csv
+rm -rf $out/unet $out/stf $out/cfg5 $out/pk $out/aug
+fi
 if [ -z "$SKIP_PMC" ]; then
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_unet --steps 3 --warmup 1
 bash tools/pmc_passes.sh gpurun_out/prof_$tag/pmc_stf --model stf --steps 3 --warmup 1
@@ -49,10 +57,5 @@ python3 tools/pmc_summary.py gpurun_out/prof_$tag/pmc_stf --batch 16 \
   --workload "cfg3 STFLSTMUNet(T=8) 256x256 train step" \
   --command "bash tools/pmc_passes.sh OUT --model stf --steps 3 --warmup 1" --json $out/pmc_traffic_stf256_t8_b16.json > $out/pmc_stf256_t8_b16_summary.txt
 fi
-cp $out/unet/run_kernel_stats.csv $out/unet256_b64_kernel_stats.csv
-cp $out/stf/run_kernel_stats.csv $out/stf256_t8_b16_kernel_stats.csv
-cp $out/cfg5/run_kernel_stats.csv $out/cfg5_stf512_t32pk_b4_fp16_kernel_stats.csv
-cp $out/pk/run_kernel_stats.csv $out/pk_fit256_kernel_stats.csv
-cp $out/aug/run_kernel_stats.csv $out/aug_b16_kernel_stats.csv
-rm -rf $out/unet $out/stf $out/cfg5 $out/pk $out/aug $out/pmc_unet $out/pmc_stf $out/mfma_unet $out/mfma_stf
+rm -rf $out/pmc_unet $out/pmc_stf $out/mfma_unet $out/mfma_stf
 ls $out
