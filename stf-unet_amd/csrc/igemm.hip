@@ -654,6 +654,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 || (BM == 128 && BN == 
   // r = y + pad (mod 2), s = x + pad (mod 2).  Rows are ordered by class (y & 1, x & 1),
   // each block lies in one class and walks only that class's taps (1/2/2/4 of the nine
   // for 3x3, none for the odd classes of 1x1) instead of masking 3/4 of the MFMAs to zero.
+  // par == 2 (an accumulating launch): classes without taps (the odd ones of a 1x1 / stride-2
+  // transposed gather) add nothing -- they get no blocks at all (stf_igemm counts the same way)
   int pcls = -1, py = 0, px = 0, Hc = 0, Wc = 0, r0 = 0, s0 = 0;
   if (TRANS && a.par) {
     int b = gtile;
@@ -662,6 +664,8 @@ __global__ __launch_bounds__(64 * WM * WN, (WM * WN == 4 || (BM == 128 && BN == 
       const int c = 3 - ci;                         // (1,1) first: 4 taps, then 2, 2, 1 (shorter tail)
       const int hc = (a.Hd - (c >> 1) + 1) >> 1, wc = (a.Wd - (c & 1) + 1) >> 1;
       const int mc = a.N * hc * wc, nb = (mc + BM - 1) / BM;
+      const int ntap = ((a.R - (((c >> 1) + a.pad) & 1) + 1) >> 1) * ((a.S - (((c & 1) + a.pad) & 1) + 1) >> 1);
+      if (a.par == 2 && ntap == 0) continue;
       if (pcls < 0) {
         if (b < nb) { pcls = c; Hc = hc; Wc = wc; m0 = b * BM; m_end = min(m0 + BM, mc); }
         else b -= nb;
@@ -967,19 +971,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // instructions over the taps only moves the stall into the taps: the DMA path itself
   // is the limit, fewer bytes per FLOP is what would help.
   constexpr bool STAGGER = STAGES == 2 && NW == 8;
-  // DEFB (2-stage kernels with the fused BN-backward reduction, single-image tiles): the y tile
-  // the reduction needs is still LDS-DMA'd into the stage just consumed at the end of the item,
-  // but nobody waits for it there: the sums run after the NEXT stage-start barrier, whose vmcnt
-  // wait covers the y DMA (issued before the dz stores), so its latency hides behind the stage
-  // transition.  The partials go to spare weight rows of that stage (rows 9*64.. of a stage,
-  // which the weight DMA never fills) and are folded after one more barrier, before any wave
-  // refills the stage.  (Same-box A/B, profiles/r04/ab_halo_epilogue.txt: the halo dgrads -1 %;
-  // deferring the output stores of the other direct epilogues into the next stage's taps instead
-  // cost +5 % -- they compete with the stage's DMA for the vector-memory address path -- and a
-  // barrier-free statistics fold was neutral: neither is built.)
-  constexpr bool DEFB = STAGES == 2 && NW == 8 && DIRECT == 1 && BNR && DIAG == 0 && IX == 1;
-  static_assert(!DEFB || (WROWS - 9 * BN) * 64 >= NW * 2 * 64 * 4, "spare weight rows for the partials");
-  static_assert(!DEFB || NW * 3 * 64 * 4 * 2 + PX * 128 <= (HROWS + 9 * BN) * 64, "y tile below the spare rows");
   static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
   static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE && NW * 3 * 64 * 4 * 2 + PX * 128 <= STAGE, "epilogue scratch");
   static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
@@ -1012,10 +1003,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // of the stage only streams the halo (half the DMA instructions at 64 source channels).
   int wkey0 = -1, wkey1 = -1;
   auto issue_part = [&](int item, int cc, int buf, bool live, int k0, int k1, bool wload) {
-    // DEFB: the lane terms of the DMA addresses are recomputed per fill rather than hoisted out
-    // of the stage loop by the compiler (the registers the deferred reduction keeps live)
-    int sub = lane >> 2, slot = lane & 3;
-    if constexpr (DEFB) asm volatile("" : "+v"(sub), "+v"(slot));
     const int nt = item / ntiles, tile = item - nt * ntiles;
     const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
@@ -1040,7 +1027,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
       if (HI + i < k0 || HI + i >= k1 || !wload) continue;
-      if (DEFB && (wave * WI + i) * RPI >= 9 * BN) continue;   // wholly past the rows: keep the spare rows
       const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
@@ -1108,84 +1094,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   }
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
   bool wl_next = true;                                   // the next fill streams weight rows too
-  uint4 uq[2][TM];                                       // direct epilogue: the packed outputs
-  int mq[TM];                                            // ... and their pixel rows (-1: outside)
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  auto red_d = [&](int rb) { return reinterpret_cast<float*>(smem + rb * STAGE + (HROWS + 9 * BN) * 64); };
-  auto fold_stats = [&](const float* red, int key) {
-    if (tid < 128) {
-      const int q = tid >> 6, col = tid & 63;
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
-      if (key != run_key) {
-        if (run_key >= 0) flush();
-        run_key = key;
-        run = 0.f;
-      }
-      run += t;
-    }
-  };
-  // DEFB state: bpend = an item's packed dz (uq, mq) and its y tile (LDS stage bbuf) wait for the
-  // next stage-start barrier; its BN affine (scale, shift, mean, invstd) of this lane's channel
-  bool bpend = false;
-  int bbuf = 0, bkey = 0, bitem = 0;
-  auto bnr_finish = [&]() {
-    {                                                    // the pixel rows again (4 registers fewer live)
-      const int nt = bitem / ntiles, tile = bitem - nt * ntiles;
-      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) mq[i] = halo_pixel<PH, PW, IX>(wave * WTM + i * 16 + fr, tq * IX, ty, tx, a.Hd, a.Wd);
-    }
-    // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat) per channel, as the in-item epilogue below
-    char* sb = smem + bbuf * STAGE;
-    const float* aff = reinterpret_cast<const float*>(sb + NW * 2 * 64 * 4) + wave * 256;
-    const char* yl = sb + NW * 3 * 64 * 4 * 2 + wave * WTM * 128;
-    float* red = red_d(bbuf);
-    auto aff8 = [&](int k, int c0, float* v) {
-      const float4 lo = *reinterpret_cast<const float4*>(aff + k * 64 + c0);
-      const float4 hi = *reinterpret_cast<const float4*>(aff + k * 64 + c0 + 4);
-      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    };
-    const bool norelu = !a.bnr_relu;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float q1[8], q2[8], sc[8], sh[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { q1[e] = 0.f; q2[e] = 0.f; }
-      aff8(0, h * 32 + fk * 8, sc);
-      aff8(1, h * 32 + fk * 8, sh);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float g[8], yv[8];
-        unpack8(uq[h][i], g);
-        const int r = i * 16 + fr;
-        unpack8(*reinterpret_cast<const uint4*>(yl + r * 128 + (((h * 4 + fk) ^ (r & 7)) << 4)), yv);
-        const bool valid = mq[i] >= 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool keep = valid & (norelu | (yv[e] * sc[e] + sh[e] > 0.f));
-          const float gg = keep ? g[e] : 0.f;
-          q1[e] += gg;
-          q2[e] += gg * yv[e];
-        }
-      }
-      float mu[8], is[8], v[16];
-      aff8(2, h * 32 + fk * 8, mu);
-      aff8(3, h * 32 + fk * 8, is);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] = q1[e];
-        v[8 + e] = is[e] * (q2[e] - mu[e] * q1[e]);
-      }
-      red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = row16_reduce_scatter(v, fr);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                        // every wave's partials are in, its y reads done
-    fold_stats(red, bkey);
-    bpend = false;
-  };
-
   // DIAG 4: per-wave cycle buckets (s_memtime) -- DMA wait, barrier, DMA issue, taps, epilogue
   uint64_t tb[5] = {0, 0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
@@ -1222,9 +1130,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       epi = false;
       __builtin_amdgcn_s_barrier();
       stamp(1);
-      if constexpr (DEFB) {
-        if (bpend) bnr_finish();                         // the vmcnt wait above covered the y DMA
-      }
       load_bias();
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
@@ -1312,6 +1217,9 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
       const __amdgpu_buffer_rsrc_t rs_dst =
           __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      uint4 uq[2][TM];
+      int mq[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int p = wave * WTM + i * 16 + fr;
@@ -1369,18 +1277,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
               mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
         }
-      if constexpr (DEFB) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) aff[k * 64 + lane] = aff_pre[k];   // read back by this wave only
-        bpend = true;
-        bbuf = buf;
-        bkey = (img / ipg) * NTn + nt;
-        bitem = cit;
-        ccc = 0;
-        ++cit;
-        epi = true;
-        continue;
-      }
       if constexpr (BNR) {
         // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat), like stf_bn_bwd_reduce
 #pragma unroll
@@ -1571,13 +1467,6 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       ccc = 0;
       ++cit;
       epi = true;
-    }
-  }
-  if constexpr (DEFB) {
-    if (bpend) {                                         // the last item's y tile and reduction
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NSTORE) : "memory");
-      __builtin_amdgcn_s_barrier();
-      bnr_finish();
     }
   }
   if (sbuf && tid < 128 && run_key >= 0) flush();
@@ -1877,6 +1766,11 @@ bool dma_enabled() {
   return on;
 }
 
+bool small_gemm_a() {
+  static const bool on = [] { const char* e = getenv("STF_SMALL_GEMM"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 // which kernel runs: 'R' = register-staged (BM 256 for Nout <= 64, else 128), or a DMA config letter
 char choose(const stf_igemm_args* a, bool dma_ok) {
   const stf_conv_geom& c = a->g;
@@ -1917,6 +1811,12 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
     const long M = (long)c.N * c.Hd * c.Wd;
     const long blocks_c = ((M + 255) / 256) * ((a->Nout + 255) / 256);
     if (a->Nout % 256 == 0 && blocks_c >= 240) return 'C';
+    // small output, long K (the STF LSTMs' hoisted backward steps dh = dgates W_hh: M = pixels of
+    // one step, K = 4C): the 256x128 tile leaves < 64 workgroups and its BK = 64 caps the split-K at
+    // K / 512; the 128x128 BK = 32 tile splits K twice as far (ksplit_of) and fills the chip.
+    // STF_SMALL_GEMM=0: the 256x128 tile (A/B).
+    const long blocks_b = ((M + 255) / 256) * ((a->Nout + 127) / 128);
+    if (a->Nout % 128 == 0 && blocks_b < 64 && (long)c.R * c.S * c.Cs >= 1024 && small_gemm_a()) return 'A';
     if (a->Nout % 128 == 0) return 'B';
     if (a->Nout == 64) return 'D';
   }
@@ -2267,10 +2167,16 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   static const bool par_on = [] { const char* e = getenv("STF_TRANS_PAR"); return !(e && e[0] == '0'); }();
   if (par_on && c.transposed && c.stride == 2 && (k == 'A' || k == 'E') && g.Mg == g.M) {
     const int bmp = cfg_of(k).bm;
+    // accumulating: tap-less classes add nothing, skip them (STF_TRANS_SKIP=0: launch them, A/B)
+    static const bool skip_on = [] { const char* e = getenv("STF_TRANS_SKIP"); return !(e && e[0] == '0'); }();
+    const int par = a->accumulate && skip_on ? 2 : 1;
     long blocks = 0;
-    for (int cl = 0; cl < 4; ++cl)
+    for (int cl = 0; cl < 4; ++cl) {
+      const int ntap = ((c.R - (((cl >> 1) + c.pad) & 1) + 1) >> 1) * ((c.S - (((cl & 1) + c.pad) & 1) + 1) >> 1);
+      if (par == 2 && ntap == 0) continue;
       blocks += ((long)c.N * ((c.Hd - (cl >> 1) + 1) >> 1) * ((c.Wd - (cl & 1) + 1) >> 1) + bmp - 1) / bmp;
-    g.par = 1;
+    }
+    g.par = par;
     g.tpg = (int)blocks;
   }
   const int ks = ksplit_of(a);
