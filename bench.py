@@ -330,6 +330,9 @@ def main():
         else:
             dist.init_process_group(backend)
     torch.cuda.set_device(dev)
+    if os.environ.get("STF_MAIN_PRIO") == "1":
+        # A/B knob: the step's main stream at high priority (the side streams stay at 0)
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
 
     from stfunet import engine, nhwc, plan
     from stfunet.ddp import GradAllReduce

@@ -47,34 +47,20 @@ int tiles_per_group(long units_per_group, int groups) {
 // group.  With G > 1 the running statistics must see the G updates in order:
 // each block parks (mean, biased var) in row 0 of its group (scratch) and
 // bn_running_kernel applies them sequentially.
-__global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __restrict__ stats, int S, int T, int G, int C,
-                                                        long Mg, const float* gamma, const float* beta, float mom,
-                                                        float eps, float* rm, float* rv, float* mean, float* invstd,
-                                                        float* scale, float* shift) {
-  __shared__ double red[stf::FOLD_NT];
-  const int g = blockIdx.y;
-  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
-  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
-  double mu = 0.0, var = 1.0;
-  float* base = stats ? stats + (size_t)g * T * 2 * C : nullptr;
-  if (stats) {
-    double s1, s2;
-    stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
-    mu = s1 / Mg;
-    var = s2 / Mg - mu * mu;
-    if (var < 0) var = 0;
-  } else if (lead) {                     // eval mode: running statistics, no update
-    mu = rm ? rm[c] : 0.f;
-    var = rv ? rv[c] : 1.f;
-  }
-  if (!lead) return;
+// the training-mode finalize of channel c of group g from its folded (sum, sum of squares);
+// shared by bn_finalize_kernel and the fused consumer (bn_act_g_kernel<., true>)
+STF_DEV void bn_fin_fwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
+                            const float* gamma, const float* beta, float mom, float eps, float* rm, float* rv,
+                            float* mean, float* invstd, float* scale, float* shift) {
+  const double mu = s1 / Mg;
+  double var = s2 / Mg - mu * mu;
+  if (var < 0) var = 0;
   const float inv = (float)(1.0 / sqrt(var + (double)eps));
   const float sc = gamma[c] * inv;
   mean[g * C + c] = (float)mu;
   invstd[g * C + c] = inv;
   scale[g * C + c] = sc;
   shift[g * C + c] = beta[c] - (float)mu * sc;
-  if (!stats) return;
   if (G == 1) {
     if (!rm) return;
     const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
@@ -84,6 +70,31 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __rest
     base[c] = (float)mu;
     base[C + c] = (float)var;
   }
+}
+
+__global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __restrict__ stats, int S, int T, int G, int C,
+                                                        long Mg, const float* gamma, const float* beta, float mom,
+                                                        float eps, float* rm, float* rv, float* mean, float* invstd,
+                                                        float* scale, float* shift) {
+  __shared__ double red[stf::FOLD_NT];
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
+  if (stats) {
+    float* base = stats + (size_t)g * T * 2 * C;
+    double s1, s2;
+    stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
+    if (lead) bn_fin_fwd_out(base, g, c, G, C, Mg, s1, s2, gamma, beta, mom, eps, rm, rv, mean, invstd, scale, shift);
+    return;
+  }
+  if (!lead) return;                     // eval mode: running statistics, no update
+  const double mu = rm ? rm[c] : 0.f, var = rv ? rv[c] : 1.f;
+  const float inv = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * inv;
+  mean[g * C + c] = (float)mu;
+  invstd[g * C + c] = inv;
+  scale[g * C + c] = sc;
+  shift[g * C + c] = beta[c] - (float)mu * sc;
 }
 
 __global__ void bn_running_kernel(const float* __restrict__ stats, int T, int G, int C, long Mg, float mom,
@@ -383,18 +394,11 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
 // Grid = (channel chunks of 16) x G.  dgamma/dbeta are summed over the groups
 // (one BatchNorm module, G calls): with G > 1 each block parks its group's sums
 // in row 0 of the group and bn_bwd_groupsum_kernel adds them in order.
-__global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
-                                                            int C, long Mg, const float* gamma, const float* mean,
-                                                            const float* invstd, float* dgamma, float* dbeta,
-                                                            float* coef) {
-  __shared__ double red[stf::FOLD_NT];
-  const int g = blockIdx.y;
-  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
-  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
-  float* base = partial + (size_t)g * T * 2 * C;
-  double s1, s2;
-  stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
-  if (!lead) return;
+// dy = A g + B y + C coefficients of channel c of group g from its folded (sum g, sum g*xhat);
+// shared by bn_bwd_finalize_kernel and the fused consumer (bn_bwd_apply_g_kernel<., true>)
+STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
+                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                            float* coef) {
   const double is = invstd[g * C + c];
   const double A = (double)gamma[c] * is;
   const double B = -A * is * s2 / Mg;
@@ -409,6 +413,20 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __
     base[c] = (float)s1;
     base[C + c] = (float)s2;
   }
+}
+
+__global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
+                                                            int C, long Mg, const float* gamma, const float* mean,
+                                                            const float* invstd, float* dgamma, float* dbeta,
+                                                            float* coef) {
+  __shared__ double red[stf::FOLD_NT];
+  const int g = blockIdx.y;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C, lead = cok && (threadIdx.x >> 4) == 0;
+  float* base = partial + (size_t)g * T * 2 * C;
+  double s1, s2;
+  stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
+  if (lead) bn_fin_bwd_out(base, g, c, G, C, Mg, s1, s2, gamma, mean, invstd, dgamma, dbeta, coef);
 }
 
 // Deferred running-statistics updates of many grouped BatchNorms in one launch
@@ -523,15 +541,101 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* 
 // (checked by the launchers).  Unit u of group g: pixel g * Mg + (u >> cgs), chunk u & (CG - 1).
 constexpr int UPT = 4;
 
-template <bool RES>
+// ------------------------------------------------------------------ finalize fused into the consumer
+// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  sync[g * 4 + 0..3] = ticket, chunks published,
+// blocks done, sticky timeout flag.  Every block of group g takes a ticket as it starts; tickets
+// 0..ceil(C/16)-1 (blocks already resident, so nothing they wait on can be starved) fold the
+// 16-channel chunks (fold16_pair_256: the separate finalize kernel's order, bit-identical) and
+// publish them with an agent-scope release; all blocks then wait for the group's chunks
+// (acquire) before they read scale/shift or the coefficients.  The group's last block to
+// finish restores the three counters to zero for the next launch.
+struct FinFwd {
+  float* stats; int S, T, C; long Mg; const float* gamma; const float* beta; float mom, eps;
+  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* sync;
+};
+struct FinBwd {
+  float* partial; int S, T, C; long Mg; const float* gamma; const float* mean; const float* invstd;
+  float* dgamma; float* dbeta; float* coef; unsigned* sync;
+};
+constexpr unsigned FIN_SPIN_LIMIT = 1u << 24;     // ~seconds of s_sleep: a wait that long is a bug
+
+template <class Chunk>
+STF_DEV void fin_prologue(unsigned* sy, int C, Chunk&& chunk) {
+  __shared__ unsigned s_ticket;
+  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(&sy[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned ticket = s_ticket, nch = (unsigned)(C + 15) / 16;
+  if (ticket < nch) {
+    unsigned mine = 0;
+    for (unsigned k = ticket; k < nch; k += gridDim.x, ++mine) {
+      chunk((int)k);
+      __syncthreads();                   // the fold's LDS is reused by the next chunk
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&sy[1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(&sy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FIN_SPIN_LIMIT) {
+        __hip_atomic_store(&sy[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+STF_DEV void fin_epilogue(unsigned* sy) {
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&sy[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    __hip_atomic_store(&sy[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sy[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sy[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+STF_DEV void fin_fwd(const FinFwd& f, int g) {
+  __shared__ double red[2 * 16 * 16];
+  float* base = f.stats + (size_t)g * f.T * 2 * f.C;
+  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+    const int c = k * 16 + (threadIdx.x & 15);
+    const bool cok = c < f.C;
+    double s1, s2;
+    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
+    if (cok && threadIdx.x < 16)
+      bn_fin_fwd_out(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv, f.mean,
+                     f.invstd, f.scale, f.shift);
+  });
+}
+
+STF_DEV void fin_bwd(const FinBwd& f, int g) {
+  __shared__ double red[2 * 16 * 16];
+  float* base = f.partial + (size_t)g * f.T * 2 * f.C;
+  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+    const int c = k * 16 + (threadIdx.x & 15);
+    const bool cok = c < f.C;
+    double s1, s2;
+    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
+    if (cok && threadIdx.x < 16)
+      bn_fin_bwd_out(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta,
+                     f.coef);
+  });
+}
+
+// FIN: scale/shift are written by this launch (fin_fwd) before they are read
+template <bool RES, bool FIN>
 __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
-                                                      const float* __restrict__ scale,
-                                                      const float* __restrict__ shift, int relu, int res_mode,
-                                                      const uint16_t* __restrict__ res, int rcs,
+                                                      const float* scale, const float* shift, int relu,
+                                                      int res_mode, const uint16_t* __restrict__ res, int rcs,
                                                       const float* __restrict__ rscale,
                                                       const float* __restrict__ rshift, uint16_t* __restrict__ out,
-                                                      int ocs) {
+                                                      int ocs, FinFwd fin) {
   const int g = blockIdx.y, C = 8 << cgs;
+  if (FIN) fin_fwd(fin, g);
   const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & ((1 << cgs) - 1);
@@ -579,6 +683,7 @@ __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict
       *reinterpret_cast<uint4*>(out + (p0 + (uk >> cgs)) * ocs + cg * 8) = pack8(v);
     }
   }
+  if (FIN) fin_epilogue(fin.sync + 4 * g);
 }
 
 // mask_mode 0: none, 1: relu(y*scale+shift) > 0, 2: mask_src > 0; same sums as bn_bwd_reduce_kernel
@@ -652,15 +757,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_g_kernel(const uint16_t* __r
 }
 
 // dy = A*g' + B*y + C (as bn_bwd_apply_kernel); bias_partial rows = g * gridDim.x + blockIdx.x
-template <bool MASK>
+// FIN: coef is written by this launch (fin_bwd) before it is read
+template <bool MASK, bool FIN>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in, int gcs,
                                                             const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
-                                                            const float* __restrict__ coef,
-                                                            const float* __restrict__ mscale,
+                                                            const float* coef, const float* __restrict__ mscale,
                                                             const float* __restrict__ mshift, uint16_t* dy,
-                                                            int dycs, float* __restrict__ bias_partial) {
+                                                            int dycs, float* __restrict__ bias_partial, FinBwd fin) {
   __shared__ float red[NT][9];
   const int g = blockIdx.y, CG = 1 << cgs, C = 8 << cgs;
+  if (FIN) fin_bwd(fin, g);
   const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & (CG - 1);
@@ -701,6 +807,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in
       *reinterpret_cast<uint4*>(dy + (p0 + (uk >> cgs)) * dycs + cg * 8) = pack8(gv);
     }
   }
+  if (FIN) fin_epilogue(fin.sync + 4 * g);
   if (!bias_partial) return;
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = sb[j];
@@ -918,13 +1025,13 @@ extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int
     const int cgs = log2i(C / 8);
     const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
     if (res)
-      hipLaunchKernelGGL(bn_act_g_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg, cgs,
-                         scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale, res_shift,
-                         (uint16_t*)out, out_cstride);
+      hipLaunchKernelGGL((bn_act_g_kernel<true, false>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+                         (int)Mg, cgs, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
+                         res_shift, (uint16_t*)out, out_cstride, FinFwd{});
     else
-      hipLaunchKernelGGL(bn_act_g_kernel<false>, grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg, cgs,
-                         scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
-                         (const float*)nullptr, (uint16_t*)out, out_cstride);
+      hipLaunchKernelGGL((bn_act_g_kernel<false, false>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+                         (int)Mg, cgs, scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
+                         (const float*)nullptr, (uint16_t*)out, out_cstride, FinFwd{});
     STF_CHECK_LAUNCH();
     return 0;
   }
@@ -1057,13 +1164,13 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
     const dim3 grid(tpg, groups);
     const int cgs = log2i(C / 8);
     if (mask_scale)
-      hipLaunchKernelGGL(bn_bwd_apply_g_kernel<true>, grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<true, false>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
                          (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
-                         dy_cstride, bias_partial);
+                         dy_cstride, bias_partial, FinBwd{});
     else
-      hipLaunchKernelGGL(bn_bwd_apply_g_kernel<false>, grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<false, false>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
                          (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
-                         dy_cstride, bias_partial);
+                         dy_cstride, bias_partial, FinBwd{});
     tiles = tpg * groups;
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
@@ -1076,6 +1183,71 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
     hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+// ---- finalize fused into its consumer (include/stfunet.h, ABI v13)
+extern "C" int stf_bn_fin_ok(int64_t M, int C, int groups) {
+  return groups >= 1 && C % 8 == 0 && M % groups == 0 && bn_g_ok(M / groups, C) ? 1 : 0;
+}
+
+extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride, int N, int H, int W, int relu,
+                              const void* res, int res_cstride, const float* res_scale, const float* res_shift,
+                              void* out, int out_cstride, stf_stream_t stream) {
+  if (!f || !f->stats || !f->sync || !f->gamma || !f->beta || !f->mean || !f->invstd || !f->scale || !f->shift)
+    return STF_EINVAL;
+  const int C = f->C, groups = f->groups;
+  const long M = (long)N * H * W;
+  if (f->M != M || f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || N % groups || y_cstride % 8 || out_cstride % 8)
+    return STF_EINVAL;
+  if (res && res_cstride % 8) return STF_EINVAL;
+  if (groups > 1 && f->running_mean) return STF_EINVAL;   // grouped running stats: parked (stf_bn_running_batch)
+  hipStream_t s = (hipStream_t)stream;
+  const long Mg = M / groups;
+  const int S = stf::colsum_stage1(f->stats, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
+  const FinFwd fin{f->stats, S, f->tiles, C, Mg, f->gamma, f->beta, f->momentum, f->eps, f->running_mean,
+                   f->running_var, f->mean, f->invstd, f->scale, f->shift, f->sync};
+  const int cgs = log2i(C / 8);
+  const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
+  const int res_mode = res ? (res_scale ? 2 : 1) : 0;
+  if (res)
+    hipLaunchKernelGGL((bn_act_g_kernel<true, true>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg,
+                       cgs, f->scale, f->shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
+                       res_shift, (uint16_t*)out, out_cstride, fin);
+  else
+    hipLaunchKernelGGL((bn_act_g_kernel<false, true>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg,
+                       cgs, f->scale, f->shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
+                       (const float*)nullptr, (uint16_t*)out, out_cstride, fin);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* f, const void* g, int g_cstride, const void* y,
+                                    int y_cstride, const float* mask_scale, const float* mask_shift, void* dy,
+                                    int dy_cstride, stf_stream_t stream) {
+  if (!f || !f->partial || !f->sync || !f->gamma || !f->mean || !f->invstd || !f->coef) return STF_EINVAL;
+  const int C = f->C, groups = f->groups;
+  const long M = f->M;
+  if (f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8)
+    return STF_EINVAL;
+  if ((mask_scale == nullptr) != (mask_shift == nullptr)) return STF_EINVAL;
+  if (groups > 1 && (f->dgamma || f->dbeta)) return STF_EINVAL;  // grouped: parked (stf_bn_groupsum_batch)
+  hipStream_t s = (hipStream_t)stream;
+  const long Mg = M / groups;
+  const int S = stf::colsum_stage1(f->partial, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
+  const FinBwd fin{f->partial, S, f->tiles, C, Mg, f->gamma, f->mean, f->invstd, f->dgamma, f->dbeta, f->coef,
+                   f->sync};
+  const int cgs = log2i(C / 8);
+  const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
+  if (mask_scale)
+    hipLaunchKernelGGL((bn_bwd_apply_g_kernel<true, true>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                       (const uint16_t*)y, y_cstride, (int)Mg, cgs, f->coef, mask_scale, mask_shift, (uint16_t*)dy,
+                       dy_cstride, (float*)nullptr, fin);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_g_kernel<false, true>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+                       (const uint16_t*)y, y_cstride, (int)Mg, cgs, f->coef, mask_scale, mask_shift, (uint16_t*)dy,
+                       dy_cstride, (float*)nullptr, fin);
+  STF_CHECK_LAUNCH();
   return 0;
 }
 

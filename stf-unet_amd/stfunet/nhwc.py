@@ -543,17 +543,62 @@ def channel_sum(x: Feat, out):
 
 # ------------------------------------------------------------------ BatchNorm
 class BNState:
-    """Per-forward BatchNorm quantities ([groups][C] each) kept for backward."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups", "training")
+    """Per-forward BatchNorm quantities ([groups][C] each) kept for backward.
+
+    A training-mode finalize may be left *pending* (bn_finalize with the fused path on):
+    the BatchNorm's consumer pass (bn_act) then runs it in its own launch
+    (stf_bn_act_fin).  Reading mean / invstd / scale / shift while it is pending runs
+    the separate finalize first, so every other reader sees the finished values."""
+    __slots__ = ("_mean", "_invstd", "_scale", "_shift", "M", "groups", "training", "_pending")
 
     def __init__(self, C, device, M, groups=1, training=True):
         t = empty((4, groups, C), torch.float32, device)
-        self.mean, self.invstd, self.scale, self.shift = t.unbind(0)
+        self._mean, self._invstd, self._scale, self._shift = t.unbind(0)
         self.M = M
         self.groups = groups
         # training: normalised with the batch statistics (mean / invstd above); eval:
         # with the running statistics, which the backward treats as constants
         self.training = training
+        self._pending = None
+
+    def materialize(self):
+        """Run a pending finalize as its own launch (stf_bn_finalize)."""
+        pend, self._pending = self._pending, None
+        if pend is not None:
+            _FIN_PENDING.pop(id(self), None)
+            d, _stats = pend
+            call("stf_bn_finalize", d.stats, d.tiles, d.groups, d.C, d.M, d.gamma, d.beta, d.momentum, d.eps,
+                 d.running_mean, d.running_var, d.mean, d.invstd, d.scale, d.shift, stream())
+
+    def take_pending(self):
+        """The pending finalize's descriptor, now owned by the caller's fused launch."""
+        pend, self._pending = self._pending, None
+        _FIN_PENDING.pop(id(self), None)
+        return pend[0]
+
+    @property
+    def mean(self):
+        if self._pending is not None:
+            self.materialize()
+        return self._mean
+
+    @property
+    def invstd(self):
+        if self._pending is not None:
+            self.materialize()
+        return self._invstd
+
+    @property
+    def scale(self):
+        if self._pending is not None:
+            self.materialize()
+        return self._scale
+
+    @property
+    def shift(self):
+        if self._pending is not None:
+            self.materialize()
+        return self._shift
 
     @staticmethod
     def identity(C, device):
@@ -565,10 +610,57 @@ class BNState:
         return st
 
 
+class _FinDesc(ctypes.Structure):      # stf_bn_fin
+    _fields_ = [("stats", ctypes.c_void_p), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
+                ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("running_mean", ctypes.c_void_p),
+                ("running_var", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("sync", ctypes.c_void_p)]
+
+
+class _BwdFinDesc(ctypes.Structure):   # stf_bn_bwd_fin
+    _fields_ = [("partial", ctypes.c_void_p), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
+                ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("mean", ctypes.c_void_p),
+                ("invstd", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("coef", ctypes.c_void_p), ("sync", ctypes.c_void_p)]
+
+
+_FIN_PENDING = {}     # id(BNState) -> BNState with a pending finalize (run at flush_batches_tracked)
+_SYNC = {}            # (id(bn module), direction, groups, device) -> persistent [groups][4] uint32 slab
+_FIN_OK = {}
+
+
+def fin_fused(M, C, groups):
+    """Whether a training BatchNorm's finalize runs inside its consumer's launch
+    (STF_BN_FIN=0: the separate stf_bn_finalize / stf_bn_bwd_finalize, A/B)."""
+    if os.environ.get("STF_BN_FIN", "1") == "0":
+        return False
+    key = (M, C, groups)
+    ok = _FIN_OK.get(key)
+    if ok is None:
+        ok = _FIN_OK[key] = bool(_lib.load().stf_bn_fin_ok(M, C, groups))
+    return ok
+
+
+def _sync_slab(bn, direction, groups, device):
+    """Counters of the fused finalize: zero when made, restored to zero by every launch,
+    so one slab per BatchNorm module and direction serves every step (and plan replays)."""
+    key = (id(bn), direction, groups, torch.device(device).index)
+    t = _SYNC.get(key)
+    if t is None:
+        t = _SYNC[key] = torch.zeros(groups * 4, dtype=torch.int32, device=device)
+    return t
+
+
+def fin_sync_timeouts():
+    """Number of fused-finalize groups whose wait ever exceeded its spin bound (sticky)."""
+    return int(sum(int((t.view(-1, 4)[:, 3] != 0).sum()) for t in _SYNC.values()))
+
+
 # num_batches_tracked increments are deferred and applied per forward with one
 # multi-tensor launch per increment value (instead of one tiny kernel per module)
 _NBT_PENDING = {}
-_RUN_PENDING = []      # (stf_bn_run_desc, stats slab kept alive until the flush)
+_RUN_PENDING = []      # (stf_bn_run_desc, (stats slab, running_mean, running_var) kept alive until the flush)
 _GSUM_PENDING = []     # (stf_bn_gsum_desc, partial slab)
 
 
@@ -586,6 +678,8 @@ class _GsumDesc(ctypes.Structure):
 def flush_batches_tracked():
     """End of a training forward: the deferred running-statistics updates of the
     grouped BatchNorms (one stf_bn_running_batch launch) and num_batches_tracked."""
+    for st in list(_FIN_PENDING.values()):      # finalizes no consumer fused (running stats, parked rows)
+        st.materialize()
     if _RUN_PENDING:
         arr = (_RunDesc * len(_RUN_PENDING))(*[d for d, _ in _RUN_PENDING])
         call("stf_bn_running_batch", arr, len(_RUN_PENDING), stream())
@@ -607,7 +701,11 @@ def flush_bn_grads():
 
 def bn_finalize(stats, tiles, bn, M, training, groups=1):
     """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats (its
-    num_batches_tracked advances by ``groups`` at flush_batches_tracked())."""
+    num_batches_tracked advances by ``groups`` at flush_batches_tracked()).
+    Training mode with the fused path (fin_fused): the finalize is left pending on the
+    returned BNState and runs inside the consumer's launch (bn_act), or on the first read
+    of its mean / invstd / scale / shift, or at flush_batches_tracked() -- the running
+    statistics are final once one of those has happened."""
     C = bn.num_features
     st = BNState(C, bn.weight.device, M, groups, training)
     mom = 0.1 if bn.momentum is None else bn.momentum
@@ -617,12 +715,22 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
         # grouped: (mean, var) of every group stay parked in the slab; the running
         # stats advance group by group in ONE batched launch at the end of forward
         _RUN_PENDING.append((_RunDesc(stats.data_ptr(), rm.data_ptr(), rv.data_ptr(), M // groups, tiles, groups, C,
-                                      float(mom)), stats))
+                                      float(mom)), (stats, rm, rv)))
         rm = rv = None
-    call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, bn.weight.data_ptr(),
-         bn.bias.data_ptr(), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
-         _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
-         stream())
+    if training and fin_fused(M, C, groups):
+        # left pending: bn_act runs it inside its own launch (stf_bn_act_fin), any other
+        # reader of the BNState through a separate stf_bn_finalize (BNState.materialize)
+        d = _FinDesc(stats.data_ptr(), tiles, groups, C, M, bn.weight.data_ptr(), bn.bias.data_ptr(), float(mom),
+                     float(bn.eps), _p(rm) if rm is not None else None, _p(rv) if rv is not None else None,
+                     _p(st._mean), _p(st._invstd), _p(st._scale), _p(st._shift),
+                     _sync_slab(bn, "f", groups, bn.weight.device).data_ptr())
+        st._pending = (d, stats)
+        _FIN_PENDING[id(st)] = st
+    else:
+        call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, bn.weight.data_ptr(),
+             bn.bias.data_ptr(), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
+             _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
+             stream())
     if training and bn.track_running_stats:
         _NBT_PENDING.setdefault(groups, []).append(bn.num_batches_tracked)
     return st
@@ -640,6 +748,14 @@ def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None, res:
     if res is not None:
         res.check()
         assert (res.N, res.H, res.W, res.C) == (y.N, y.H, y.W, y.C)
+    if st._pending is not None and pooled is None:
+        rsc = _p(res_st.scale) if res_st is not None else None       # (a pending residual BN runs first)
+        rsh = _p(res_st.shift) if res_st is not None else None
+        d = st.take_pending()
+        call("stf_bn_act_fin", ctypes.byref(d), y.ptr(), y.cs, y.N, y.H, y.W, int(relu),
+             res.ptr() if res is not None else None, res.cs if res is not None else 0, rsc, rsh, out.ptr(), out.cs,
+             stream())
+        return
     call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, st.groups, _p(st.scale), _p(st.shift), int(relu),
          res.ptr() if res is not None else None, res.cs if res is not None else 0,
          _p(res_st.scale) if res_st is not None else None, _p(res_st.shift) if res_st is not None else None,
@@ -761,6 +877,19 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                         dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
         dgamma = dbeta = None
+    if st.training and dbias is None and fin_fused(y.M, C, G):
+        # finalize + apply in one launch (stf_bn_bwd_apply_fin)
+        dst = out if out is not None else g
+        if out is not None:
+            out.check()
+            assert (out.N, out.H, out.W, out.C) == (y.N, y.H, y.W, C)
+        if mask_relu:
+            assert out is not None
+        d = _BwdFinDesc(_p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean), _p(st.invstd), _p(dgamma),
+                        _p(dbeta), _p(coef), _sync_slab(bn, "b", G, dev).data_ptr())
+        call("stf_bn_bwd_apply_fin", ctypes.byref(d), g.ptr(), g.cs, y.ptr(), y.cs,
+             _p(st.scale) if mask_relu else None, _p(st.shift) if mask_relu else None, dst.ptr(), dst.cs, stream())
+        return dst
     call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     if not st.training:

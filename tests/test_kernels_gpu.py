@@ -361,11 +361,13 @@ def test_bn_forward_backward(pool, C):
     s2 = (y * y).sum((0, 2, 3))
     stats = torch.stack([s, s2]).contiguous().view(-1)
     st = nhwc.bn_finalize(stats, 1, m.bn, yf.M, training=True)
-    assert rel(m.bn.running_mean, ref_bn.running_mean) < 1e-5
-    assert rel(m.bn.running_var, ref_bn.running_var) < 1e-5
     out = nhwc.zeros_feat(2, H, H, 2 * C, DEV)
     pooled = nhwc.new_feat(2, H // 2, H // 2, C, DEV) if pool else None
     nhwc.bn_act(yf, st, out.slice(C, C), pooled=pooled)
+    # (the finalize may run inside bn_act's launch: the running stats are final once the
+    # BNState has been consumed -- or at nhwc.flush_batches_tracked())
+    assert rel(m.bn.running_mean, ref_bn.running_mean) < 1e-5
+    assert rel(m.bn.running_var, ref_bn.running_var) < 1e-5
     assert rel(out.dense()[:, C:], a_ref) < 1e-2
     if pool:
         # pool the bf16-rounded activations (straight-through) so ties break like the kernel
