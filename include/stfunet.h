@@ -283,7 +283,8 @@ typedef struct stf_bn_bwd_fin {
 int stf_bn_fin_ok(int64_t M, int C, int groups);
 int stf_bn_act_fin(const stf_bn_fin* fin, const void* y, int y_cstride, int N, int H, int W,
                    int relu, const void* res, int res_cstride, const float* res_scale,
-                   const float* res_shift, void* out, int out_cstride, stf_stream_t stream);
+                   const float* res_shift, void* out, int out_cstride, void* pooled,
+                   stf_stream_t stream);   /* pooled (as stf_bn_act): groups == 1 only */
 int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* fin, const void* g, int g_cstride, const void* y,
                          int y_cstride, const float* mask_scale, const float* mask_shift, void* dy,
                          int dy_cstride, stf_stream_t stream);

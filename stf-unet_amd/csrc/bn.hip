@@ -33,6 +33,23 @@ STF_DEV void load_affine(const float* p, int c, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// Device-coherent (agent-scope, relaxed) accesses for values one workgroup publishes to the others
+// of the same launch (the fused finalize): these loads / stores go to the coherence point per
+// instruction, so neither side needs an agent-scope fence -- a release fence writes back, and an
+// acquire fence invalidates, the whole L2 of the XCD, which thousands of workgroups per launch
+// cannot afford.
+STF_DEV void store_coh(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+STF_DEV void load_affine_coh(const float* p, int c, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = __hip_atomic_load(const_cast<float*>(p) + c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool COH>
+STF_DEV void load_aff(const float* p, int c, float (&v)[8]) {
+  if (COH) load_affine_coh(p, c, v);
+  else load_affine(p, c, v);
+}
+
 int tiles_per_group(long units_per_group, int groups) {
   long t = (units_per_group + NT - 1) / NT;
   const long cap = (1024 + groups - 1) / groups;    // <= FOLD16_ROWS partial rows per group
@@ -49,6 +66,8 @@ int tiles_per_group(long units_per_group, int groups) {
 // bn_running_kernel applies them sequentially.
 // the training-mode finalize of channel c of group g from its folded (sum, sum of squares);
 // shared by bn_finalize_kernel and the fused consumer (bn_act_g_kernel<., true>)
+// COH: scale / shift are read by the other workgroups of the same (fused) launch
+template <bool COH>
 STF_DEV void bn_fin_fwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
                             const float* gamma, const float* beta, float mom, float eps, float* rm, float* rv,
                             float* mean, float* invstd, float* scale, float* shift) {
@@ -59,8 +78,13 @@ STF_DEV void bn_fin_fwd_out(float* base, int g, int c, int G, int C, long Mg, do
   const float sc = gamma[c] * inv;
   mean[g * C + c] = (float)mu;
   invstd[g * C + c] = inv;
-  scale[g * C + c] = sc;
-  shift[g * C + c] = beta[c] - (float)mu * sc;
+  if (COH) {
+    store_coh(scale + g * C + c, sc);
+    store_coh(shift + g * C + c, beta[c] - (float)mu * sc);
+  } else {
+    scale[g * C + c] = sc;
+    shift[g * C + c] = beta[c] - (float)mu * sc;
+  }
   if (G == 1) {
     if (!rm) return;
     const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
@@ -84,7 +108,8 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __rest
     float* base = stats + (size_t)g * T * 2 * C;
     double s1, s2;
     stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
-    if (lead) bn_fin_fwd_out(base, g, c, G, C, Mg, s1, s2, gamma, beta, mom, eps, rm, rv, mean, invstd, scale, shift);
+    if (lead)
+      bn_fin_fwd_out<false>(base, g, c, G, C, Mg, s1, s2, gamma, beta, mom, eps, rm, rv, mean, invstd, scale, shift);
     return;
   }
   if (!lead) return;                     // eval mode: running statistics, no update
@@ -113,15 +138,141 @@ __global__ void bn_running_kernel(const float* __restrict__ stats, int T, int G,
   rv[c] = run_v;
 }
 
+// dy = A g + B y + C coefficients of channel c of group g from its folded (sum g, sum g*xhat);
+// shared by bn_bwd_finalize_kernel and the fused consumer (bn_bwd_apply_g_kernel<., true>)
+// COH: coef is read by the other workgroups of the same (fused) launch
+template <bool COH>
+STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
+                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                            float* coef) {
+  const double is = invstd[g * C + c];
+  const double A = (double)gamma[c] * is;
+  const double B = -A * is * s2 / Mg;
+  const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
+  if (COH) {
+    store_coh(coef + (size_t)g * 3 * C + c, (float)A);
+    store_coh(coef + (size_t)g * 3 * C + C + c, (float)B);
+    store_coh(coef + (size_t)g * 3 * C + 2 * C + c, (float)Cc);
+  } else {
+    coef[(size_t)g * 3 * C + c] = (float)A;
+    coef[(size_t)g * 3 * C + C + c] = (float)B;
+    coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
+  }
+  if (G == 1) {
+    if (dgamma) dgamma[c] = (float)s2;
+    if (dbeta) dbeta[c] = (float)s1;
+  } else {
+    base[c] = (float)s1;
+    base[C + c] = (float)s2;
+  }
+}
+
+// ------------------------------------------------------------------ finalize fused into the consumer
+// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  sync[g * 4 + 0..3] = ticket, chunks published,
+// blocks done, sticky timeout flag.  Every block of group g takes a ticket as it starts; tickets
+// 0..ceil(C/16)-1 (blocks already resident, so nothing they wait on can be starved) fold the
+// 16-channel chunks (fold16_pair_256: the separate finalize kernel's order, bit-identical), store
+// the values other blocks read (scale / shift, or the coefficients) device-coherent, wait for
+// those stores to complete and count the chunk; all blocks wait for the group's count, then read
+// the values device-coherent (store_coh / load_affine_coh: no agent-scope fences, whose L2
+// writeback / invalidate per block measured 2x the whole step).  The group's last block to finish
+// restores the three counters to zero for the next launch.
+struct FinFwd {
+  float* stats; int S, T, C; long Mg; const float* gamma; const float* beta; float mom, eps;
+  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* sync;
+};
+struct FinBwd {
+  float* partial; int S, T, C; long Mg; const float* gamma; const float* mean; const float* invstd;
+  float* dgamma; float* dbeta; float* coef; unsigned* sync;
+};
+constexpr unsigned FIN_SPIN_LIMIT = 1u << 24;     // ~seconds of s_sleep: a wait that long is a bug
+
+template <class Chunk>
+STF_DEV void fin_prologue(unsigned* sy, int C, Chunk&& chunk) {
+  __shared__ unsigned s_ticket;
+  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(&sy[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned ticket = s_ticket, nch = (unsigned)(C + 15) / 16;
+  if (ticket < nch) {
+    unsigned mine = 0;
+    for (unsigned k = ticket; k < nch; k += gridDim.x, ++mine) {
+      chunk((int)k);
+      __syncthreads();                   // the fold's LDS is reused by the next chunk
+    }
+    // the chunk's published values were stored device-coherent: complete them, then count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&sy[1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(&sy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FIN_SPIN_LIMIT) {
+        __hip_atomic_store(&sy[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();                       // (the published values are then read device-coherent)
+}
+
+STF_DEV void fin_epilogue(unsigned* sy) {
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&sy[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    __hip_atomic_store(&sy[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sy[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&sy[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+STF_DEV void fin_fwd(const FinFwd& f, int g) {
+  __shared__ double red[2 * 16 * 16];
+  float* base = f.stats + (size_t)g * f.T * 2 * f.C;
+  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+    const int c = k * 16 + (threadIdx.x & 15);
+    const bool cok = c < f.C;
+    double s1, s2;
+    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
+    if (cok && threadIdx.x < 16)
+      bn_fin_fwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv, f.mean,
+                     f.invstd, f.scale, f.shift);
+  });
+}
+
+STF_DEV void fin_bwd(const FinBwd& f, int g) {
+  __shared__ double red[2 * 16 * 16];
+  float* base = f.partial + (size_t)g * f.T * 2 * f.C;
+  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+    const int c = k * 16 + (threadIdx.x & 15);
+    const bool cok = c < f.C;
+    double s1, s2;
+    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
+    if (cok && threadIdx.x < 16)
+      bn_fin_bwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta,
+                     f.coef);
+  });
+}
+
 // ------------------------------------------------------------------ apply
 // res_mode 0: none, 1: + res tensor, 2: + (res*rscale[g] + rshift[g])
-template <bool POOL>
+// FIN (one statistics group): scale/shift are written by this launch (fin_fwd) before they are read
+template <bool POOL, bool FIN>
 __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, int H, int W, int C, long Mg,
-                              const float* __restrict__ scale, const float* __restrict__ shift, int relu,
-                              int res_mode, const uint16_t* __restrict__ res, int rcs,
-                              const float* __restrict__ rscale, const float* __restrict__ rshift,
-                              uint16_t* __restrict__ out, int ocs, uint16_t* __restrict__ pooled) {
+                              const float* scale, const float* shift, int relu, int res_mode,
+                              const uint16_t* __restrict__ res, int rcs, const float* __restrict__ rscale,
+                              const float* __restrict__ rshift, uint16_t* __restrict__ out, int ocs,
+                              uint16_t* __restrict__ pooled, FinFwd fin) {
   const int CG = C / 8;
+  // FIN (launched with one group only): a thread's channel chunk is fixed (the grid stride is a
+  // multiple of C / 8), so its affine is read once, device-coherent, after the finalize
+  float fsc[8], fsh[8];
+  if (FIN) {
+    fin_fwd(fin, 0);
+    const int cg0 = (int)((blockIdx.x * (long)NT + threadIdx.x) % CG);
+    load_affine_coh(scale, cg0 * 8, fsc);
+    load_affine_coh(shift, cg0 * 8, fsh);
+  }
   const long units = POOL ? N * (H / 2) * (W / 2) * CG : N * H * W * CG;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
     const int cg = (int)(u % CG);
@@ -129,8 +280,13 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
     if (!POOL) {
       const int g = (int)(pix / Mg);
       float sc[8], sh[8], v[8];
-      load_affine(scale + (size_t)g * C, cg * 8, sc);
-      load_affine(shift + (size_t)g * C, cg * 8, sh);
+      if (FIN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sc[j] = fsc[j]; sh[j] = fsh[j]; }
+      } else {
+        load_affine(scale + (size_t)g * C, cg * 8, sc);
+        load_affine(shift + (size_t)g * C, cg * 8, sh);
+      }
       unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
@@ -159,8 +315,13 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
       const int py = rem / Wp, px = rem - py * Wp;
       const int g = (int)(n * H * W / Mg);
       float sc[8], sh[8], mx[8];
-      load_affine(scale + (size_t)g * C, cg * 8, sc);
-      load_affine(shift + (size_t)g * C, cg * 8, sh);
+      if (FIN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sc[j] = fsc[j]; sh[j] = fsh[j]; }
+      } else {
+        load_affine(scale + (size_t)g * C, cg * 8, sc);
+        load_affine(shift + (size_t)g * C, cg * 8, sh);
+      }
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const long p = (n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
@@ -178,6 +339,7 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
       *reinterpret_cast<uint4*>(pooled + pix * C + cg * 8) = pack8(mx);
     }
   }
+  if (FIN) fin_epilogue(fin.sync);
 }
 
 // ------------------------------------------------------------------ backward reduce
@@ -394,27 +556,6 @@ __global__ __launch_bounds__(PNT) void bn_bwd_reduce_pool_kernel(const uint16_t*
 // Grid = (channel chunks of 16) x G.  dgamma/dbeta are summed over the groups
 // (one BatchNorm module, G calls): with G > 1 each block parks its group's sums
 // in row 0 of the group and bn_bwd_groupsum_kernel adds them in order.
-// dy = A g + B y + C coefficients of channel c of group g from its folded (sum g, sum g*xhat);
-// shared by bn_bwd_finalize_kernel and the fused consumer (bn_bwd_apply_g_kernel<., true>)
-STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
-                            const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                            float* coef) {
-  const double is = invstd[g * C + c];
-  const double A = (double)gamma[c] * is;
-  const double B = -A * is * s2 / Mg;
-  const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
-  coef[(size_t)g * 3 * C + c] = (float)A;
-  coef[(size_t)g * 3 * C + C + c] = (float)B;
-  coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
-  if (G == 1) {
-    if (dgamma) dgamma[c] = (float)s2;
-    if (dbeta) dbeta[c] = (float)s1;
-  } else {
-    base[c] = (float)s1;
-    base[C + c] = (float)s2;
-  }
-}
-
 __global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __restrict__ partial, int S, int T, int G,
                                                             int C, long Mg, const float* gamma, const float* mean,
                                                             const float* invstd, float* dgamma, float* dbeta,
@@ -426,7 +567,7 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __
   float* base = partial + (size_t)g * T * 2 * C;
   double s1, s2;
   stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
-  if (lead) bn_fin_bwd_out(base, g, c, G, C, Mg, s1, s2, gamma, mean, invstd, dgamma, dbeta, coef);
+  if (lead) bn_fin_bwd_out<false>(base, g, c, G, C, Mg, s1, s2, gamma, mean, invstd, dgamma, dbeta, coef);
 }
 
 // Deferred running-statistics updates of many grouped BatchNorms in one launch
@@ -541,91 +682,6 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* 
 // (checked by the launchers).  Unit u of group g: pixel g * Mg + (u >> cgs), chunk u & (CG - 1).
 constexpr int UPT = 4;
 
-// ------------------------------------------------------------------ finalize fused into the consumer
-// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  sync[g * 4 + 0..3] = ticket, chunks published,
-// blocks done, sticky timeout flag.  Every block of group g takes a ticket as it starts; tickets
-// 0..ceil(C/16)-1 (blocks already resident, so nothing they wait on can be starved) fold the
-// 16-channel chunks (fold16_pair_256: the separate finalize kernel's order, bit-identical) and
-// publish them with an agent-scope release; all blocks then wait for the group's chunks
-// (acquire) before they read scale/shift or the coefficients.  The group's last block to
-// finish restores the three counters to zero for the next launch.
-struct FinFwd {
-  float* stats; int S, T, C; long Mg; const float* gamma; const float* beta; float mom, eps;
-  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* sync;
-};
-struct FinBwd {
-  float* partial; int S, T, C; long Mg; const float* gamma; const float* mean; const float* invstd;
-  float* dgamma; float* dbeta; float* coef; unsigned* sync;
-};
-constexpr unsigned FIN_SPIN_LIMIT = 1u << 24;     // ~seconds of s_sleep: a wait that long is a bug
-
-template <class Chunk>
-STF_DEV void fin_prologue(unsigned* sy, int C, Chunk&& chunk) {
-  __shared__ unsigned s_ticket;
-  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(&sy[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const unsigned ticket = s_ticket, nch = (unsigned)(C + 15) / 16;
-  if (ticket < nch) {
-    unsigned mine = 0;
-    for (unsigned k = ticket; k < nch; k += gridDim.x, ++mine) {
-      chunk((int)k);
-      __syncthreads();                   // the fold's LDS is reused by the next chunk
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(&sy[1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(&sy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > FIN_SPIN_LIMIT) {
-        __hip_atomic_store(&sy[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-STF_DEV void fin_epilogue(unsigned* sy) {
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(&sy[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-    __hip_atomic_store(&sy[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&sy[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&sy[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-STF_DEV void fin_fwd(const FinFwd& f, int g) {
-  __shared__ double red[2 * 16 * 16];
-  float* base = f.stats + (size_t)g * f.T * 2 * f.C;
-  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
-    const int c = k * 16 + (threadIdx.x & 15);
-    const bool cok = c < f.C;
-    double s1, s2;
-    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
-    if (cok && threadIdx.x < 16)
-      bn_fin_fwd_out(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv, f.mean,
-                     f.invstd, f.scale, f.shift);
-  });
-}
-
-STF_DEV void fin_bwd(const FinBwd& f, int g) {
-  __shared__ double red[2 * 16 * 16];
-  float* base = f.partial + (size_t)g * f.T * 2 * f.C;
-  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
-    const int c = k * 16 + (threadIdx.x & 15);
-    const bool cok = c < f.C;
-    double s1, s2;
-    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
-    if (cok && threadIdx.x < 16)
-      bn_fin_bwd_out(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta,
-                     f.coef);
-  });
-}
-
 // FIN: scale/shift are written by this launch (fin_fwd) before they are read
 template <bool RES, bool FIN>
 __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
@@ -640,8 +696,8 @@ __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & ((1 << cgs) - 1);
   float sc[8], sh[8], rs[8], rh[8];
-  load_affine(scale + (size_t)g * C, cg * 8, sc);
-  load_affine(shift + (size_t)g * C, cg * 8, sh);
+  load_aff<FIN>(scale + (size_t)g * C, cg * 8, sc);
+  load_aff<FIN>(shift + (size_t)g * C, cg * 8, sh);
   if (RES && res_mode == 2) {
     load_affine(rscale + (size_t)g * C, cg * 8, rs);
     load_affine(rshift + (size_t)g * C, cg * 8, rh);
@@ -771,9 +827,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & (CG - 1);
   float A[8], B[8], Cc[8], ms[8], mh[8];
-  load_affine(coef + (size_t)g * 3 * C, cg * 8, A);
-  load_affine(coef + (size_t)g * 3 * C + C, cg * 8, B);
-  load_affine(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
+  load_aff<FIN>(coef + (size_t)g * 3 * C, cg * 8, A);
+  load_aff<FIN>(coef + (size_t)g * 3 * C + C, cg * 8, B);
+  load_aff<FIN>(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
   if (MASK) {
     load_affine(mscale + (size_t)g * C, cg * 8, ms);
     load_affine(mshift + (size_t)g * C, cg * 8, mh);
@@ -1036,13 +1092,14 @@ extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int
     return 0;
   }
   if (pooled)
-    hipLaunchKernelGGL(bn_act_kernel<true>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (long)N, H,
-                       W, C, Mg, scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
-                       (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled);
+    hipLaunchKernelGGL((bn_act_kernel<true, false>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+                       (long)N, H, W, C, Mg, scale, shift, relu, 0, (const uint16_t*)nullptr, 0,
+                       (const float*)nullptr, (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled,
+                       FinFwd{});
   else
-    hipLaunchKernelGGL(bn_act_kernel<false>, dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (long)N,
-                       H, W, C, Mg, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
-                       res_shift, (uint16_t*)out, out_cstride, (uint16_t*)nullptr);
+    hipLaunchKernelGGL((bn_act_kernel<false, false>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+                       (long)N, H, W, C, Mg, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride,
+                       res_scale, res_shift, (uint16_t*)out, out_cstride, (uint16_t*)nullptr, FinFwd{});
   STF_CHECK_LAUNCH();
   return 0;
 }
@@ -1193,20 +1250,31 @@ extern "C" int stf_bn_fin_ok(int64_t M, int C, int groups) {
 
 extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride, int N, int H, int W, int relu,
                               const void* res, int res_cstride, const float* res_scale, const float* res_shift,
-                              void* out, int out_cstride, stf_stream_t stream) {
+                              void* out, int out_cstride, void* pooled, stf_stream_t stream) {
   if (!f || !f->stats || !f->sync || !f->gamma || !f->beta || !f->mean || !f->invstd || !f->scale || !f->shift)
     return STF_EINVAL;
   const int C = f->C, groups = f->groups;
   const long M = (long)N * H * W;
   if (f->M != M || f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || N % groups || y_cstride % 8 || out_cstride % 8)
     return STF_EINVAL;
-  if (res && res_cstride % 8) return STF_EINVAL;
+  if (res && (res_cstride % 8 || pooled)) return STF_EINVAL;
+  if (pooled && (((H | W) & 1) || groups != 1)) return STF_EINVAL;   // pooled: one statistics group
   if (groups > 1 && f->running_mean) return STF_EINVAL;   // grouped running stats: parked (stf_bn_running_batch)
   hipStream_t s = (hipStream_t)stream;
   const long Mg = M / groups;
   const int S = stf::colsum_stage1(f->stats, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
   const FinFwd fin{f->stats, S, f->tiles, C, Mg, f->gamma, f->beta, f->momentum, f->eps, f->running_mean,
                    f->running_var, f->mean, f->invstd, f->scale, f->shift, f->sync};
+  if (pooled) {
+    const long units = (long)N * (H / 2) * (W / 2) * (C / 8);
+    const long blocks = std::min<long>((units + NT - 1) / NT, 8192);
+    hipLaunchKernelGGL((bn_act_kernel<true, true>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+                       (long)N, H, W, C, Mg, f->scale, f->shift, relu, 0, (const uint16_t*)nullptr, 0,
+                       (const float*)nullptr, (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled,
+                       fin);
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
   const int cgs = log2i(C / 8);
   const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
   const int res_mode = res ? (res_scale ? 2 : 1) : 0;

@@ -1766,11 +1766,6 @@ bool dma_enabled() {
   return on;
 }
 
-bool small_gemm_a() {
-  static const bool on = [] { const char* e = getenv("STF_SMALL_GEMM"); return !(e && e[0] == '0'); }();
-  return on;
-}
-
 // which kernel runs: 'R' = register-staged (BM 256 for Nout <= 64, else 128), or a DMA config letter
 char choose(const stf_igemm_args* a, bool dma_ok) {
   const stf_conv_geom& c = a->g;
@@ -1811,12 +1806,6 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
     const long M = (long)c.N * c.Hd * c.Wd;
     const long blocks_c = ((M + 255) / 256) * ((a->Nout + 255) / 256);
     if (a->Nout % 256 == 0 && blocks_c >= 240) return 'C';
-    // small output, long K (the STF LSTMs' hoisted backward steps dh = dgates W_hh: M = pixels of
-    // one step, K = 4C): the 256x128 tile leaves < 64 workgroups and its BK = 64 caps the split-K at
-    // K / 512; the 128x128 BK = 32 tile splits K twice as far (ksplit_of) and fills the chip.
-    // STF_SMALL_GEMM=0: the 256x128 tile (A/B).
-    const long blocks_b = ((M + 255) / 256) * ((a->Nout + 127) / 128);
-    if (a->Nout % 128 == 0 && blocks_b < 64 && (long)c.R * c.S * c.Cs >= 1024 && small_gemm_a()) return 'A';
     if (a->Nout % 128 == 0) return 'B';
     if (a->Nout == 64) return 'D';
   }

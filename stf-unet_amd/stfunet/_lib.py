@@ -83,7 +83,7 @@ _SIGS = {
     "stf_bn_bwd_apply_tiles": (c_int, [c_int64, c_int]),
     "stf_bn_bwd_apply": (c_int, [P, c_int, P, c_int, c_int64, c_int, c_int, P, P, P, P, c_int, P, P, P]),
     "stf_bn_fin_ok": (c_int, [c_int64, c_int, c_int]),
-    "stf_bn_act_fin": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P]),
+    "stf_bn_act_fin": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P, P]),
     "stf_bn_bwd_apply_fin": (c_int, [P, P, c_int, P, c_int, P, P, P, c_int, P]),
     "stf_head_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "stf_head_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P, P, P]),

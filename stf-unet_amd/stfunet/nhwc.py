@@ -631,9 +631,11 @@ _FIN_OK = {}
 
 
 def fin_fused(M, C, groups):
-    """Whether a training BatchNorm's finalize runs inside its consumer's launch
-    (STF_BN_FIN=0: the separate stf_bn_finalize / stf_bn_bwd_finalize, A/B)."""
-    if os.environ.get("STF_BN_FIN", "1") == "0":
+    """Whether a training BatchNorm's finalize runs inside its consumer's launch: opt-in
+    (STF_BN_FIN=1).  Bit-identical, but measured 1.8x slower steps (every
+    workgroup's ticket / completion atomics and polls on one device-scope address serialize at
+    the memory side, ~40-55 ns per workgroup), so the separate finalize launches stay the default."""
+    if os.environ.get("STF_BN_FIN", "0") != "1":
         return False
     key = (M, C, groups)
     ok = _FIN_OK.get(key)
@@ -748,13 +750,13 @@ def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None, res:
     if res is not None:
         res.check()
         assert (res.N, res.H, res.W, res.C) == (y.N, y.H, y.W, y.C)
-    if st._pending is not None and pooled is None:
+    if st._pending is not None and (pooled is None or st.groups == 1):
         rsc = _p(res_st.scale) if res_st is not None else None       # (a pending residual BN runs first)
         rsh = _p(res_st.shift) if res_st is not None else None
         d = st.take_pending()
         call("stf_bn_act_fin", ctypes.byref(d), y.ptr(), y.cs, y.N, y.H, y.W, int(relu),
              res.ptr() if res is not None else None, res.cs if res is not None else 0, rsc, rsh, out.ptr(), out.cs,
-             stream())
+             pooled.ptr() if pooled is not None else None, stream())
         return
     call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, st.groups, _p(st.scale), _p(st.shift), int(relu),
          res.ptr() if res is not None else None, res.cs if res is not None else 0,

@@ -1,5 +1,5 @@
 """BatchNorm finalize fused into its consumer pass (stf_bn_act_fin / stf_bn_bwd_apply_fin,
-ABI v13) against the separate finalize launch (STF_BN_FIN=0): bit for bit.
+ABI v13; opt-in, STF_BN_FIN=1) against the separate finalize launch: bit for bit.
 
 The fused kernels fold the partial slabs in the separate kernel's fixed fp64 order
 (reduce.h fold16_pair_256), so every output -- the normalised activation, mean / invstd /
@@ -53,6 +53,7 @@ def _stats(G, tiles, C, Mg, seed):
 def test_forward_fused_finalize_bitwise(monkeypatch, N, H, W, C, G, tiles, res):
     from stfunet import nhwc
     M = N * H * W
+    monkeypatch.setenv("STF_BN_FIN", "1")
     assert nhwc.fin_fused(M, C, G)
     y = nhwc.new_feat(N, H, W, C, DEV)
     y.buf.normal_()
@@ -90,6 +91,37 @@ def test_forward_fused_finalize_bitwise(monkeypatch, N, H, W, C, G, tiles, res):
     assert nhwc.fin_sync_timeouts() == 0
     for t in nhwc._SYNC.values():
         assert int(t.view(-1, 4)[:, :3].abs().sum()) == 0            # counters restored
+
+
+@pytest.mark.parametrize("N,H,W,C,tiles", [(2, 16, 16, 64, 5), (2, 8, 8, 512, 3), (4, 64, 64, 128, 1500)])
+def test_pooled_forward_fused_finalize_bitwise(monkeypatch, N, H, W, C, tiles):
+    """bn_act with the fused 2x2 max pool (UNet Down) and one statistics group."""
+    from stfunet import nhwc
+    M = N * H * W
+    y = nhwc.new_feat(N, H, W, C, DEV)
+    y.buf.normal_()
+    out = []
+    for mode in ("0", "1", "1"):
+        monkeypatch.setenv("STF_BN_FIN", mode)
+        bn = _bn(C, 1) if mode == "0" or len(out) == 1 else bn
+        if len(out) == 2:
+            with torch.no_grad():
+                bn.running_mean.copy_(rm0)
+                bn.running_var.copy_(rv0)
+        rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+        st = nhwc.bn_finalize(_stats(1, tiles, C, M, 2), tiles, bn, M, True, 1)
+        o = nhwc.new_feat(N, H, W, C, DEV)
+        pooled = nhwc.new_feat(N, H // 2, W // 2, C, DEV)
+        nhwc.bn_act(y, st, o, relu=True, pooled=pooled)
+        assert st._pending is None
+        nhwc.flush_batches_tracked()
+        torch.cuda.synchronize()
+        out.append([o.buf.clone(), pooled.buf.clone(), st.mean.clone(), st.scale.clone(), st.shift.clone(),
+                    bn.running_mean.clone(), bn.running_var.clone()])
+    for k in (1, 2):
+        for i, (a, b) in enumerate(zip(out[0], out[k])):
+            assert torch.equal(a, b), (k, i)
+    assert nhwc.fin_sync_timeouts() == 0
 
 
 @pytest.mark.parametrize("N,H,W,C,G,tiles", SHAPES)
