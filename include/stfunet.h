@@ -246,13 +246,15 @@ int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int y_cstride,
  * stf_bn_finalize + stf_bn_act (training forward) or stf_bn_bwd_finalize + stf_bn_bwd_apply
  * (training backward), bit-identical outputs (the same fixed fp64 fold order), every side
  * output of the separate finalize written as it would be (mean/invstd/scale/shift, running
- * stats or the parked rows of a grouped BatchNorm; dgamma/dbeta or the parked sums).  The
- * first ceil(C/16) workgroups of each group to start fold one 16-channel chunk each and
- * publish it; the group's other workgroups wait for those (device-scope flags), then stream.
- * `sync` is a [groups][4] uint32 slab, zero before the first launch, restored to zero by
- * every launch (keep one per call site; launches sharing a slab must not overlap); word 3 of
- * a group turns 1 (sticky) if a wait ever exceeded its spin bound.  stf_bn_fin_ok: whether
- * (M, C, groups) takes these kernels (else STF_EINVAL: use the two-launch pair). */
+ * stats or the parked rows of a grouped BatchNorm; dgamma/dbeta or the parked sums).
+ * Workgroups 0..ceil(C/16)-1 of each group fold one 16-channel chunk each and publish it by a
+ * per-chunk flag set to the current epoch; the group's other workgroups wait for the flags
+ * (device-coherent polls), then stream.  `flags` is a per-call-site slab of
+ * stf_bn_fin_flags_words(C, groups) uint32 (zero-initialised once; the last word turns 1,
+ * sticky, if a wait ever exceeded its spin bound); `epoch` a device uint32 that
+ * stf_bn_fin_epoch_bump advances: bump it between two launches that use the same flags slab
+ * (stream-ordered).  stf_bn_fin_ok: whether (M, C, groups) takes these kernels (else
+ * STF_EINVAL: use the two-launch pair). */
 typedef struct stf_bn_fin {
   float* stats;                /* [groups][tiles][2][C] (stf_bn_finalize's stats) */
   int tiles, groups, C;
@@ -266,7 +268,8 @@ typedef struct stf_bn_fin {
   float* invstd;
   float* scale;
   float* shift;
-  unsigned* sync;
+  unsigned* flags;
+  const unsigned* epoch;
 } stf_bn_fin;
 typedef struct stf_bn_bwd_fin {
   float* partial;              /* [groups][tiles][2][C] (stf_bn_bwd_finalize's partial) */
@@ -278,9 +281,12 @@ typedef struct stf_bn_bwd_fin {
   float* dgamma;               /* NULL with groups > 1: parked for stf_bn_groupsum_batch */
   float* dbeta;
   float* coef;                 /* [groups][3][C], written */
-  unsigned* sync;
+  unsigned* flags;
+  const unsigned* epoch;
 } stf_bn_bwd_fin;
 int stf_bn_fin_ok(int64_t M, int C, int groups);
+int stf_bn_fin_flags_words(int C, int groups);
+int stf_bn_fin_epoch_bump(unsigned* epoch, stf_stream_t stream);
 int stf_bn_act_fin(const stf_bn_fin* fin, const void* y, int y_cstride, int N, int H, int W,
                    int relu, const void* res, int res_cstride, const float* res_scale,
                    const float* res_shift, void* out, int out_cstride, void* pooled,

@@ -168,48 +168,57 @@ STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, do
 }
 
 // ------------------------------------------------------------------ finalize fused into the consumer
-// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  sync[g * 4 + 0..3] = ticket, chunks published,
-// blocks done, sticky timeout flag.  Every block of group g takes a ticket as it starts; tickets
-// 0..ceil(C/16)-1 (blocks already resident, so nothing they wait on can be starved) fold the
-// 16-channel chunks (fold16_pair_256: the separate finalize kernel's order, bit-identical), store
-// the values other blocks read (scale / shift, or the coefficients) device-coherent, wait for
-// those stores to complete and count the chunk; all blocks wait for the group's count, then read
-// the values device-coherent (store_coh / load_affine_coh: no agent-scope fences, whose L2
-// writeback / invalidate per block measured 2x the whole step).  The group's last block to finish
-// restores the three counters to zero for the next launch.
+// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  Workgroups 0..ceil(C/16)-1 of each group fold one
+// 16-channel chunk each (fold16_pair_256: the separate finalize kernel's order, bit-identical),
+// store the values other workgroups read (scale / shift, or the coefficients) device-coherent,
+// wait for those stores and then set the chunk's flag to this launch's epoch; every workgroup
+// waits until all of its group's flags carry the epoch, then reads the values device-coherent.
+// No fences (an agent-scope release / acquire writes back / invalidates the XCD's whole L2) and no
+// per-workgroup atomics on a shared address (the memory side serializes those, ~40-55 ns per
+// workgroup: the first, ticket-based version of this protocol doubled the step time).  Deadlock
+// freedom rests on in-order workgroup dispatch: on every XCD a group's folding workgroups have
+// lower indices than its waiting ones, so they are resident before any waiter is.  The epoch is a
+// device word advanced by stf_bn_fin_epoch_bump between two launches of one call site (so the
+// flags need no reset); flags[g][k * FIN_FLAG_STRIDE], a timeout sets the sticky word err.
 struct FinFwd {
   float* stats; int S, T, C; long Mg; const float* gamma; const float* beta; float mom, eps;
-  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* sync;
+  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* flags;
+  const unsigned* epoch;
 };
 struct FinBwd {
   float* partial; int S, T, C; long Mg; const float* gamma; const float* mean; const float* invstd;
-  float* dgamma; float* dbeta; float* coef; unsigned* sync;
+  float* dgamma; float* dbeta; float* coef; unsigned* flags; const unsigned* epoch;
 };
-constexpr unsigned FIN_SPIN_LIMIT = 1u << 24;     // ~seconds of s_sleep: a wait that long is a bug
+constexpr int FIN_FLAG_STRIDE = 32;               // one 128-B line per chunk flag
+constexpr unsigned FIN_SPIN_LIMIT = 1u << 22;     // polls ~1 us apart: seconds -- a wait that long is a bug
 
+STF_DEV unsigned load_coh_u(const unsigned* p) {
+  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+STF_DEV void store_coh_u(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// flags: this group's [nch][FIN_FLAG_STRIDE]; err: the slab's sticky timeout word
 template <class Chunk>
-STF_DEV void fin_prologue(unsigned* sy, int C, Chunk&& chunk) {
-  __shared__ unsigned s_ticket;
-  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(&sy[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const unsigned ticket = s_ticket, nch = (unsigned)(C + 15) / 16;
-  if (ticket < nch) {
-    unsigned mine = 0;
-    for (unsigned k = ticket; k < nch; k += gridDim.x, ++mine) {
-      chunk((int)k);
-      __syncthreads();                   // the fold's LDS is reused by the next chunk
-    }
-    // the chunk's published values were stored device-coherent: complete them, then count
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(&sy[1], mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+STF_DEV void fin_prologue(unsigned* flags, unsigned* err, const unsigned* epoch, int C, Chunk&& chunk) {
+  const unsigned ep = load_coh_u(epoch);
+  const int nch = (C + 15) / 16;
+  for (int k = blockIdx.x; k < nch; k += gridDim.x) {
+    chunk(k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's device-coherent stores are done
+    __syncthreads();                                   // (and the fold's LDS is free for the next chunk)
+    if (threadIdx.x == 0) store_coh_u(flags + k * FIN_FLAG_STRIDE, ep);
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {                // wave 0 polls the group's flags, one per lane
     unsigned spins = 0;
-    while (__hip_atomic_load(&sy[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nch) {
-      __builtin_amdgcn_s_sleep(1);
+    for (;;) {
+      bool mine = true;
+      for (int t = threadIdx.x; t < nch; t += 64) mine = mine && load_coh_u(flags + t * FIN_FLAG_STRIDE) == ep;
+      if (__all(mine)) break;
+      __builtin_amdgcn_s_sleep(32);
       if (++spins > FIN_SPIN_LIMIT) {
-        __hip_atomic_store(&sy[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) store_coh_u(err, 1u);
         break;
       }
     }
@@ -217,41 +226,42 @@ STF_DEV void fin_prologue(unsigned* sy, int C, Chunk&& chunk) {
   __syncthreads();                       // (the published values are then read device-coherent)
 }
 
-STF_DEV void fin_epilogue(unsigned* sy) {
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(&sy[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
-    __hip_atomic_store(&sy[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&sy[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&sy[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
+STF_DEV int fin_nch(int C) { return (C + 15) / 16; }
 
 STF_DEV void fin_fwd(const FinFwd& f, int g) {
   __shared__ double red[2 * 16 * 16];
   float* base = f.stats + (size_t)g * f.T * 2 * f.C;
-  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+  const int nch = fin_nch(f.C);
+  fin_prologue(f.flags + (size_t)g * nch * FIN_FLAG_STRIDE, f.flags + (size_t)gridDim.y * nch * FIN_FLAG_STRIDE,
+               f.epoch, f.C, [&](int k) {
     const int c = k * 16 + (threadIdx.x & 15);
     const bool cok = c < f.C;
     double s1, s2;
     stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
     if (cok && threadIdx.x < 16)
-      bn_fin_fwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv, f.mean,
-                     f.invstd, f.scale, f.shift);
+      bn_fin_fwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv,
+                           f.mean, f.invstd, f.scale, f.shift);
   });
 }
 
 STF_DEV void fin_bwd(const FinBwd& f, int g) {
   __shared__ double red[2 * 16 * 16];
   float* base = f.partial + (size_t)g * f.T * 2 * f.C;
-  fin_prologue(f.sync + 4 * g, f.C, [&](int k) {
+  const int nch = fin_nch(f.C);
+  fin_prologue(f.flags + (size_t)g * nch * FIN_FLAG_STRIDE, f.flags + (size_t)gridDim.y * nch * FIN_FLAG_STRIDE,
+               f.epoch, f.C, [&](int k) {
     const int c = k * 16 + (threadIdx.x & 15);
     const bool cok = c < f.C;
     double s1, s2;
     stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
     if (cok && threadIdx.x < 16)
       bn_fin_bwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta,
-                     f.coef);
+                           f.coef);
   });
+}
+
+__global__ void fin_epoch_bump_kernel(unsigned* epoch) {
+  if (threadIdx.x == 0) epoch[0] = epoch[0] + 1u;
 }
 
 // ------------------------------------------------------------------ apply
@@ -339,7 +349,6 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
       *reinterpret_cast<uint4*>(pooled + pix * C + cg * 8) = pack8(mx);
     }
   }
-  if (FIN) fin_epilogue(fin.sync);
 }
 
 // ------------------------------------------------------------------ backward reduce
@@ -739,7 +748,6 @@ __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict
       *reinterpret_cast<uint4*>(out + (p0 + (uk >> cgs)) * ocs + cg * 8) = pack8(v);
     }
   }
-  if (FIN) fin_epilogue(fin.sync + 4 * g);
 }
 
 // mask_mode 0: none, 1: relu(y*scale+shift) > 0, 2: mask_src > 0; same sums as bn_bwd_reduce_kernel
@@ -863,7 +871,6 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in
       *reinterpret_cast<uint4*>(dy + (p0 + (uk >> cgs)) * dycs + cg * 8) = pack8(gv);
     }
   }
-  if (FIN) fin_epilogue(fin.sync + 4 * g);
   if (!bias_partial) return;
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = sb[j];
@@ -1248,10 +1255,20 @@ extern "C" int stf_bn_fin_ok(int64_t M, int C, int groups) {
   return groups >= 1 && C % 8 == 0 && M % groups == 0 && bn_g_ok(M / groups, C) ? 1 : 0;
 }
 
+extern "C" int stf_bn_fin_flags_words(int C, int groups) { return groups * ((C + 15) / 16) * FIN_FLAG_STRIDE + 1; }
+
+extern "C" int stf_bn_fin_epoch_bump(unsigned* epoch, stf_stream_t stream) {
+  if (!epoch) return STF_EINVAL;
+  hipLaunchKernelGGL(fin_epoch_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, epoch);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride, int N, int H, int W, int relu,
                               const void* res, int res_cstride, const float* res_scale, const float* res_shift,
                               void* out, int out_cstride, void* pooled, stf_stream_t stream) {
-  if (!f || !f->stats || !f->sync || !f->gamma || !f->beta || !f->mean || !f->invstd || !f->scale || !f->shift)
+  if (!f || !f->stats || !f->flags || !f->epoch || !f->gamma || !f->beta || !f->mean || !f->invstd || !f->scale ||
+      !f->shift)
     return STF_EINVAL;
   const int C = f->C, groups = f->groups;
   const long M = (long)N * H * W;
@@ -1264,7 +1281,7 @@ extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride,
   const long Mg = M / groups;
   const int S = stf::colsum_stage1(f->stats, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
   const FinFwd fin{f->stats, S, f->tiles, C, Mg, f->gamma, f->beta, f->momentum, f->eps, f->running_mean,
-                   f->running_var, f->mean, f->invstd, f->scale, f->shift, f->sync};
+                   f->running_var, f->mean, f->invstd, f->scale, f->shift, f->flags, f->epoch};
   if (pooled) {
     const long units = (long)N * (H / 2) * (W / 2) * (C / 8);
     const long blocks = std::min<long>((units + NT - 1) / NT, 8192);
@@ -1293,7 +1310,7 @@ extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride,
 extern "C" int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* f, const void* g, int g_cstride, const void* y,
                                     int y_cstride, const float* mask_scale, const float* mask_shift, void* dy,
                                     int dy_cstride, stf_stream_t stream) {
-  if (!f || !f->partial || !f->sync || !f->gamma || !f->mean || !f->invstd || !f->coef) return STF_EINVAL;
+  if (!f || !f->partial || !f->flags || !f->epoch || !f->gamma || !f->mean || !f->invstd || !f->coef) return STF_EINVAL;
   const int C = f->C, groups = f->groups;
   const long M = f->M;
   if (f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8)
@@ -1304,7 +1321,7 @@ extern "C" int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* f, const void* g, int 
   const long Mg = M / groups;
   const int S = stf::colsum_stage1(f->partial, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
   const FinBwd fin{f->partial, S, f->tiles, C, Mg, f->gamma, f->mean, f->invstd, f->dgamma, f->dbeta, f->coef,
-                   f->sync};
+                   f->flags, f->epoch};
   const int cgs = log2i(C / 8);
   const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
   if (mask_scale)

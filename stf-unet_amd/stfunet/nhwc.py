@@ -615,26 +615,28 @@ class _FinDesc(ctypes.Structure):      # stf_bn_fin
                 ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
                 ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("running_mean", ctypes.c_void_p),
                 ("running_var", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
-                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("sync", ctypes.c_void_p)]
+                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("epoch", ctypes.c_void_p)]
 
 
 class _BwdFinDesc(ctypes.Structure):   # stf_bn_bwd_fin
     _fields_ = [("partial", ctypes.c_void_p), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
                 ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("mean", ctypes.c_void_p),
                 ("invstd", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
-                ("coef", ctypes.c_void_p), ("sync", ctypes.c_void_p)]
+                ("coef", ctypes.c_void_p), ("flags", ctypes.c_void_p), ("epoch", ctypes.c_void_p)]
 
 
 _FIN_PENDING = {}     # id(BNState) -> BNState with a pending finalize (run at flush_batches_tracked)
-_SYNC = {}            # (id(bn module), direction, groups, device) -> persistent [groups][4] uint32 slab
+_SYNC = {}            # (id(bn module), direction, groups, C, device) -> persistent flags slab (uint32)
+_SLAB_USE = {}        # same key -> host epoch count of its last launch
+_EPOCH = {}           # device index -> [device epoch word (int32, starts at 1), host count of bumps]
 _FIN_OK = {}
 
 
 def fin_fused(M, C, groups):
     """Whether a training BatchNorm's finalize runs inside its consumer's launch: opt-in
-    (STF_BN_FIN=1).  Bit-identical, but measured 1.8x slower steps (every
-    workgroup's ticket / completion atomics and polls on one device-scope address serialize at
-    the memory side, ~40-55 ns per workgroup), so the separate finalize launches stay the default."""
+    (STF_BN_FIN=1), bit-identical to the separate stf_bn_finalize / stf_bn_bwd_finalize
+    launches (DESIGN.md section 5.1 for the measurements)."""
     if os.environ.get("STF_BN_FIN", "0") != "1":
         return False
     key = (M, C, groups)
@@ -644,19 +646,44 @@ def fin_fused(M, C, groups):
     return ok
 
 
-def _sync_slab(bn, direction, groups, device):
-    """Counters of the fused finalize: zero when made, restored to zero by every launch,
-    so one slab per BatchNorm module and direction serves every step (and plan replays)."""
-    key = (id(bn), direction, groups, torch.device(device).index)
+def _epoch(device):
+    key = torch.device(device).index
+    e = _EPOCH.get(key)
+    if e is None:
+        # 1, not 0: a fresh (zeroed) flags slab must not read as published
+        e = _EPOCH[key] = [torch.ones(1, dtype=torch.int32, device=device), 0]
+    return e
+
+
+def fin_epoch_begin(device):
+    """Start a new fused-finalize epoch (the programs call this at the top of every forward and
+    backward, inside what the launch plans record, so each call site's flags slab is used at most
+    once per epoch in replays too)."""
+    if os.environ.get("STF_BN_FIN", "0") == "1":
+        e = _epoch(device)
+        call("stf_bn_fin_epoch_bump", e[0].data_ptr(), stream())
+        e[1] += 1
+
+
+def _fin_slab(bn, direction, C, groups, device):
+    """(flags slab, epoch word) for one fused launch; a second launch of the same call site in one
+    epoch (a caller outside the programs) starts a new epoch first."""
+    key = (id(bn), direction, groups, C, torch.device(device).index)
     t = _SYNC.get(key)
     if t is None:
-        t = _SYNC[key] = torch.zeros(groups * 4, dtype=torch.int32, device=device)
-    return t
+        t = _SYNC[key] = torch.zeros(_lib.load().stf_bn_fin_flags_words(C, groups), dtype=torch.int32,
+                                     device=device)
+    e = _epoch(device)
+    if _SLAB_USE.get(key) == e[1]:
+        call("stf_bn_fin_epoch_bump", e[0].data_ptr(), stream())
+        e[1] += 1
+    _SLAB_USE[key] = e[1]
+    return t.data_ptr(), e[0].data_ptr()
 
 
 def fin_sync_timeouts():
-    """Number of fused-finalize groups whose wait ever exceeded its spin bound (sticky)."""
-    return int(sum(int((t.view(-1, 4)[:, 3] != 0).sum()) for t in _SYNC.values()))
+    """Number of fused-finalize slabs whose wait ever exceeded its spin bound (sticky last word)."""
+    return int(sum(int(t[-1] != 0) for t in _SYNC.values()))
 
 
 # num_batches_tracked increments are deferred and applied per forward with one
@@ -725,7 +752,7 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
         d = _FinDesc(stats.data_ptr(), tiles, groups, C, M, bn.weight.data_ptr(), bn.bias.data_ptr(), float(mom),
                      float(bn.eps), _p(rm) if rm is not None else None, _p(rv) if rv is not None else None,
                      _p(st._mean), _p(st._invstd), _p(st._scale), _p(st._shift),
-                     _sync_slab(bn, "f", groups, bn.weight.device).data_ptr())
+                     *_fin_slab(bn, "f", C, groups, bn.weight.device))
         st._pending = (d, stats)
         _FIN_PENDING[id(st)] = st
     else:
@@ -888,7 +915,7 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         if mask_relu:
             assert out is not None
         d = _BwdFinDesc(_p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean), _p(st.invstd), _p(dgamma),
-                        _p(dbeta), _p(coef), _sync_slab(bn, "b", G, dev).data_ptr())
+                        _p(dbeta), _p(coef), *_fin_slab(bn, "b", C, G, dev))
         call("stf_bn_bwd_apply_fin", ctypes.byref(d), g.ptr(), g.cs, y.ptr(), y.cs,
              _p(st.scale) if mask_relu else None, _p(st.shift) if mask_relu else None, dst.ptr(), dst.cs, stream())
         return dst

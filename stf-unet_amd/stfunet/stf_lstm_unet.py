@@ -445,6 +445,7 @@ class STFProgram:
         """Refresh the packed weights (one launch) and run the forward schedule."""
         self.packs.refresh()
         nhwc.ACTIVE_PACKS = self.packs
+        nhwc.fin_epoch_begin(x.device)
         try:
             return self._forward(x, training, need_bwd)
         finally:
@@ -452,6 +453,7 @@ class STFProgram:
 
     def backward(self, S, dlogits):
         nhwc.ACTIVE_PACKS = self.packs
+        nhwc.fin_epoch_begin(dlogits.device)
         ws = self._wstream = nhwc.wgrad_side_stream(dlogits.device)
         nhwc.WGRAD_STREAM = ws
         nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device)

@@ -146,6 +146,7 @@ class UNetProgram:
         """Refresh the packed weights (one launch) and run the forward schedule."""
         self.packs.refresh()
         nhwc.ACTIVE_PACKS = self.packs
+        nhwc.fin_epoch_begin(x.device)
         try:
             return self._forward(x, training, need_bwd)
         finally:
@@ -156,6 +157,7 @@ class UNetProgram:
         # program) measured +1 % at cfg2 but makes every concurrent kernel's duration (and
         # so bench.py's per-kernel roofline) a shared-machine number
         nhwc.ACTIVE_PACKS = self.packs
+        nhwc.fin_epoch_begin(dlogits.device)
         ws = nhwc.wgrad_side_stream(dlogits.device) if os.environ.get("STF_UNET_WGRAD_SIDE") == "1" else None
         nhwc.WGRAD_STREAM = ws
         nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device) if ws is not None else None

@@ -5,8 +5,8 @@ The fused kernels fold the partial slabs in the separate kernel's fixed fp64 ord
 (reduce.h fold16_pair_256), so every output -- the normalised activation, mean / invstd /
 scale / shift, the running statistics (direct for one group, parked rows + the batched
 update for several), dy, dgamma / dbeta (direct, or parked + stf_bn_groupsum_batch) --
-must be identical, on a first launch and on repeated launches through the same counter slab
-(the kernels restore it to zero), including shapes where a group has fewer workgroups than
+must be identical, on a first launch and on repeated launches through the same flags slab
+(a new epoch per launch), including shapes where a group has fewer workgroups than
 16-channel chunks (one workgroup folds several) and partial slabs longer than the direct
 fold (stage-1 pre-pass).  The whole STF and UNet training steps (eager, then plan replays)
 are compared the same way.
@@ -61,7 +61,7 @@ def test_forward_fused_finalize_bitwise(monkeypatch, N, H, W, C, G, tiles, res):
     if res:
         r.buf.normal_()
     out = {}
-    for mode in ("0", "1", "1"):                      # the second fused run reuses the counter slab
+    for mode in ("0", "1", "1"):                      # the second fused run reuses the flags slab
         monkeypatch.setenv("STF_BN_FIN", mode)
         bn = _bn(C, 1)
         if mode == "1" and "1" in out:
@@ -89,8 +89,6 @@ def test_forward_fused_finalize_bitwise(monkeypatch, N, H, W, C, G, tiles, res):
         for i, (a, b) in enumerate(zip(out["0"], out[key])):
             assert torch.equal(a, b), (key, i, (a.float() - b.float()).abs().max().item())
     assert nhwc.fin_sync_timeouts() == 0
-    for t in nhwc._SYNC.values():
-        assert int(t.view(-1, 4)[:, :3].abs().sum()) == 0            # counters restored
 
 
 @pytest.mark.parametrize("N,H,W,C,tiles", [(2, 16, 16, 64, 5), (2, 8, 8, 512, 3), (4, 64, 64, 128, 1500)])
@@ -153,8 +151,6 @@ def test_backward_fused_finalize_bitwise(monkeypatch, N, H, W, C, G, tiles, mask
         for i, (a, b) in enumerate(zip(out[0], out[k])):
             assert torch.equal(a, b), (k, i, (a.float() - b.float()).abs().max().item())
     assert nhwc.fin_sync_timeouts() == 0
-    for t in nhwc._SYNC.values():
-        assert int(t.view(-1, 4)[:, :3].abs().sum()) == 0
 
 
 def _train_steps(model, x, t, steps):
