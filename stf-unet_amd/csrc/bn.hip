@@ -210,8 +210,8 @@ STF_DEV void fin_prologue(unsigned* flags, unsigned* err, const unsigned* epoch,
     __syncthreads();                                   // (and the fold's LDS is free for the next chunk)
     if (threadIdx.x == 0) store_coh_u(flags + k * FIN_FLAG_STRIDE, ep);
   }
-  if (threadIdx.x < 64) {                // wave 0 polls the group's flags, one per lane
-    unsigned spins = 0;
+  if (threadIdx.x < 64) {                // wave 0 polls the group's flags, one per lane, in parallel
+    unsigned spins = 0;                   // (walking them one by one from one lane measured slower)
     for (;;) {
       bool mine = true;
       for (int t = threadIdx.x; t < nch; t += 64) mine = mine && load_coh_u(flags + t * FIN_FLAG_STRIDE) == ep;

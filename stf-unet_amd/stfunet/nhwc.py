@@ -636,7 +636,8 @@ _FIN_OK = {}
 def fin_fused(M, C, groups):
     """Whether a training BatchNorm's finalize runs inside its consumer's launch: opt-in
     (STF_BN_FIN=1), bit-identical to the separate stf_bn_finalize / stf_bn_bwd_finalize
-    launches (DESIGN.md section 5.1 for the measurements)."""
+    launches but measured slower (cfg3 +10 %, cfg2 +4 %: the pass's workgroups wait through the
+    fold), so the separate launches are the default."""
     if os.environ.get("STF_BN_FIN", "0") != "1":
         return False
     key = (M, C, groups)
