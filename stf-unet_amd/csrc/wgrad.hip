@@ -192,7 +192,16 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
   const int per_img = tiles_y * tiles_x;
 
-  uint4 ra[CHA], rb[CHB];
+  uint4 ra[CHA], rb[CHB], rg[DIAG == 3 ? CHA : 1];
+  // DIAG 3 (timing only, results wrong): the cost side of forming dy = A g mask(y) + B y + C while
+  // staging instead of reading a materialized dy -- a second dy-sized tensor read per tile (another
+  // image's rows: not L2-hot) and the per-element transform with 40 coefficient registers live
+  // (the 5 x 64 coefficients live in LDS: 40 more registers per thread spill the kernel)
+  __shared__ float coefs[DIAG == 3 ? 5 * 64 : 1];
+  if (DIAG == 3) {
+    for (int j = tid; j < 5 * 64; j += NT) coefs[j] = (float)(a.Nout + j) * 1e-4f;
+    __syncthreads();
+  }
   auto load = [&](int t) {
     const int img = t / per_img, rem = t - img * per_img;
     // column-major: the next tile is the one below, whose halo shares two of the (PH + 2)
@@ -208,6 +217,12 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       ra[i] = make_uint4(0, 0, 0, 0);
       if (yd < a.Hd && xd < a.Wd)
         ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
+      if (DIAG == 3) {
+        const int im2 = img + 1 < a.N ? img + 1 : 0;
+        rg[i] = make_uint4(0, 0, 0, 0);
+        if (yd < a.Hd && xd < a.Wd)
+          rg[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((im2 * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
+      }
     }
 #pragma unroll
     for (int i = 0; i < CHB; ++i) {
@@ -224,6 +239,18 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
 #pragma unroll
     for (int i = 0; i < CHA; ++i) {
       const int e = tid + i * NT;
+      if (DIAG == 3) {
+        float yv[8], gv[8];
+        unpack8(ra[i], yv);
+        unpack8(rg[i], gv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float* cf = coefs + (e & 7) * 8 + j;
+          const float gj = yv[j] * cf[192] + cf[256] > 0.f ? gv[j] : 0.f;
+          yv[j] = cf[0] * gj + cf[64] * yv[j] + cf[128];
+        }
+        ra[i] = pack8(yv);
+      }
       *reinterpret_cast<uint4*>(sa + (e >> 3) * SR + (e & 7) * 8) = ra[i];
     }
 #pragma unroll
@@ -808,6 +835,8 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16 && diag == 2)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (pw == 16 && diag == 3)
+      hipLaunchKernelGGL((wgrad3x3_kernel<16, 3>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16)
       hipLaunchKernelGGL((wgrad3x3_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else
