@@ -637,7 +637,9 @@ def fin_fused(M, C, groups):
     """Whether a training BatchNorm's finalize runs inside its consumer's launch: opt-in
     (STF_BN_FIN=1), bit-identical to the separate stf_bn_finalize / stf_bn_bwd_finalize
     launches but measured slower (cfg3 +10 %, cfg2 +4 %: the pass's workgroups wait through the
-    fold), so the separate launches are the default."""
+    fold), so the separate launches are the default.  A wait that exceeds
+    its spin bound (a broken in-order-dispatch assumption) lets the launch finish with wrong
+    values and sets its slab's sticky word: fin_sync_timeouts() reports it."""
     if os.environ.get("STF_BN_FIN", "0") != "1":
         return False
     key = (M, C, groups)
