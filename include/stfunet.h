@@ -242,58 +242,6 @@ int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int y_cstride,
                      int C, int groups, const float* mask_scale, const float* mask_shift,
                      const float* coef, void* dy, int dy_cstride, float* bias_partial,
                      float* dbias, stf_stream_t stream);
-/* Finalize fused into the streaming pass that consumes it (ABI v13): one launch instead of
- * stf_bn_finalize + stf_bn_act (training forward) or stf_bn_bwd_finalize + stf_bn_bwd_apply
- * (training backward), bit-identical outputs (the same fixed fp64 fold order), every side
- * output of the separate finalize written as it would be (mean/invstd/scale/shift, running
- * stats or the parked rows of a grouped BatchNorm; dgamma/dbeta or the parked sums).
- * Workgroups 0..ceil(C/16)-1 of each group fold one 16-channel chunk each and publish it by a
- * per-chunk flag set to the current epoch; the group's other workgroups wait for the flags
- * (device-coherent polls), then stream.  `flags` is a per-call-site slab of
- * stf_bn_fin_flags_words(C, groups) uint32 (zero-initialised once; the last word turns 1,
- * sticky, if a wait ever exceeded its spin bound); `epoch` a device uint32 that
- * stf_bn_fin_epoch_bump advances: bump it between two launches that use the same flags slab
- * (stream-ordered).  stf_bn_fin_ok: whether (M, C, groups) takes these kernels (else
- * STF_EINVAL: use the two-launch pair). */
-typedef struct stf_bn_fin {
-  float* stats;                /* [groups][tiles][2][C] (stf_bn_finalize's stats) */
-  int tiles, groups, C;
-  int64_t M;
-  const float* gamma;
-  const float* beta;
-  float momentum, eps;
-  float* running_mean;         /* NULL: not tracked, or parked (groups > 1) as in stf_bn_finalize */
-  float* running_var;
-  float* mean;
-  float* invstd;
-  float* scale;
-  float* shift;
-  unsigned* flags;
-  const unsigned* epoch;
-} stf_bn_fin;
-typedef struct stf_bn_bwd_fin {
-  float* partial;              /* [groups][tiles][2][C] (stf_bn_bwd_finalize's partial) */
-  int tiles, groups, C;
-  int64_t M;
-  const float* gamma;
-  const float* mean;
-  const float* invstd;
-  float* dgamma;               /* NULL with groups > 1: parked for stf_bn_groupsum_batch */
-  float* dbeta;
-  float* coef;                 /* [groups][3][C], written */
-  unsigned* flags;
-  const unsigned* epoch;
-} stf_bn_bwd_fin;
-int stf_bn_fin_ok(int64_t M, int C, int groups);
-int stf_bn_fin_flags_words(int C, int groups);
-int stf_bn_fin_epoch_bump(unsigned* epoch, stf_stream_t stream);
-int stf_bn_act_fin(const stf_bn_fin* fin, const void* y, int y_cstride, int N, int H, int W,
-                   int relu, const void* res, int res_cstride, const float* res_scale,
-                   const float* res_shift, void* out, int out_cstride, void* pooled,
-                   stf_stream_t stream);   /* pooled (as stf_bn_act): groups == 1 only */
-int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* fin, const void* g, int g_cstride, const void* y,
-                         int y_cstride, const float* mask_scale, const float* mask_shift, void* dy,
-                         int dy_cstride, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- head + loss
  * UNet OutConv fused with the last BN+ReLU (src/unet.py:16-17,37,56):

@@ -33,23 +33,6 @@ STF_DEV void load_affine(const float* p, int c, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-// Device-coherent (agent-scope, relaxed) accesses for values one workgroup publishes to the others
-// of the same launch (the fused finalize): these loads / stores go to the coherence point per
-// instruction, so neither side needs an agent-scope fence -- a release fence writes back, and an
-// acquire fence invalidates, the whole L2 of the XCD, which thousands of workgroups per launch
-// cannot afford.
-STF_DEV void store_coh(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-STF_DEV void load_affine_coh(const float* p, int c, float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    v[j] = __hip_atomic_load(const_cast<float*>(p) + c + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool COH>
-STF_DEV void load_aff(const float* p, int c, float (&v)[8]) {
-  if (COH) load_affine_coh(p, c, v);
-  else load_affine(p, c, v);
-}
-
 int tiles_per_group(long units_per_group, int groups) {
   long t = (units_per_group + NT - 1) / NT;
   const long cap = (1024 + groups - 1) / groups;    // <= FOLD16_ROWS partial rows per group
@@ -64,10 +47,7 @@ int tiles_per_group(long units_per_group, int groups) {
 // group.  With G > 1 the running statistics must see the G updates in order:
 // each block parks (mean, biased var) in row 0 of its group (scratch) and
 // bn_running_kernel applies them sequentially.
-// the training-mode finalize of channel c of group g from its folded (sum, sum of squares);
-// shared by bn_finalize_kernel and the fused consumer (bn_act_g_kernel<., true>)
-// COH: scale / shift are read by the other workgroups of the same (fused) launch
-template <bool COH>
+// the training-mode finalize of channel c of group g from its folded (sum, sum of squares)
 STF_DEV void bn_fin_fwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
                             const float* gamma, const float* beta, float mom, float eps, float* rm, float* rv,
                             float* mean, float* invstd, float* scale, float* shift) {
@@ -78,13 +58,8 @@ STF_DEV void bn_fin_fwd_out(float* base, int g, int c, int G, int C, long Mg, do
   const float sc = gamma[c] * inv;
   mean[g * C + c] = (float)mu;
   invstd[g * C + c] = inv;
-  if (COH) {
-    store_coh(scale + g * C + c, sc);
-    store_coh(shift + g * C + c, beta[c] - (float)mu * sc);
-  } else {
-    scale[g * C + c] = sc;
-    shift[g * C + c] = beta[c] - (float)mu * sc;
-  }
+  scale[g * C + c] = sc;
+  shift[g * C + c] = beta[c] - (float)mu * sc;
   if (G == 1) {
     if (!rm) return;
     const double unb = Mg > 1 ? var * Mg / (Mg - 1) : var;
@@ -109,7 +84,7 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_finalize_kernel(float* __rest
     double s1, s2;
     stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
     if (lead)
-      bn_fin_fwd_out<false>(base, g, c, G, C, Mg, s1, s2, gamma, beta, mom, eps, rm, rv, mean, invstd, scale, shift);
+      bn_fin_fwd_out(base, g, c, G, C, Mg, s1, s2, gamma, beta, mom, eps, rm, rv, mean, invstd, scale, shift);
     return;
   }
   if (!lead) return;                     // eval mode: running statistics, no update
@@ -138,10 +113,7 @@ __global__ void bn_running_kernel(const float* __restrict__ stats, int T, int G,
   rv[c] = run_v;
 }
 
-// dy = A g + B y + C coefficients of channel c of group g from its folded (sum g, sum g*xhat);
-// shared by bn_bwd_finalize_kernel and the fused consumer (bn_bwd_apply_g_kernel<., true>)
-// COH: coef is read by the other workgroups of the same (fused) launch
-template <bool COH>
+// dy = A g + B y + C coefficients of channel c of group g from its folded (sum g, sum g*xhat)
 STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, double s1, double s2,
                             const float* gamma, const float* mean, const float* invstd, float* dgamma, float* dbeta,
                             float* coef) {
@@ -149,15 +121,9 @@ STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, do
   const double A = (double)gamma[c] * is;
   const double B = -A * is * s2 / Mg;
   const double Cc = -A * s1 / Mg + A * is * mean[g * C + c] * s2 / Mg;
-  if (COH) {
-    store_coh(coef + (size_t)g * 3 * C + c, (float)A);
-    store_coh(coef + (size_t)g * 3 * C + C + c, (float)B);
-    store_coh(coef + (size_t)g * 3 * C + 2 * C + c, (float)Cc);
-  } else {
-    coef[(size_t)g * 3 * C + c] = (float)A;
-    coef[(size_t)g * 3 * C + C + c] = (float)B;
-    coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
-  }
+  coef[(size_t)g * 3 * C + c] = (float)A;
+  coef[(size_t)g * 3 * C + C + c] = (float)B;
+  coef[(size_t)g * 3 * C + 2 * C + c] = (float)Cc;
   if (G == 1) {
     if (dgamma) dgamma[c] = (float)s2;
     if (dbeta) dbeta[c] = (float)s1;
@@ -167,122 +133,15 @@ STF_DEV void bn_fin_bwd_out(float* base, int g, int c, int G, int C, long Mg, do
   }
 }
 
-// ------------------------------------------------------------------ finalize fused into the consumer
-// (stf_bn_act_fin / stf_bn_bwd_apply_fin).  Workgroups 0..ceil(C/16)-1 of each group fold one
-// 16-channel chunk each (fold16_pair_256: the separate finalize kernel's order, bit-identical),
-// store the values other workgroups read (scale / shift, or the coefficients) device-coherent,
-// wait for those stores and then set the chunk's flag to this launch's epoch; every workgroup
-// waits until all of its group's flags carry the epoch, then reads the values device-coherent.
-// No fences (an agent-scope release / acquire writes back / invalidates the XCD's whole L2) and no
-// per-workgroup atomics on a shared address (the memory side serializes those, ~40-55 ns per
-// workgroup: the first, ticket-based version of this protocol doubled the step time).  Deadlock
-// freedom rests on in-order workgroup dispatch: on every XCD a group's folding workgroups have
-// lower indices than its waiting ones, so they are resident before any waiter is.  The epoch is a
-// device word advanced by stf_bn_fin_epoch_bump between two launches of one call site (so the
-// flags need no reset); flags[g][k * FIN_FLAG_STRIDE], a timeout sets the sticky word err.
-struct FinFwd {
-  float* stats; int S, T, C; long Mg; const float* gamma; const float* beta; float mom, eps;
-  float* rm; float* rv; float* mean; float* invstd; float* scale; float* shift; unsigned* flags;
-  const unsigned* epoch;
-};
-struct FinBwd {
-  float* partial; int S, T, C; long Mg; const float* gamma; const float* mean; const float* invstd;
-  float* dgamma; float* dbeta; float* coef; unsigned* flags; const unsigned* epoch;
-};
-constexpr int FIN_FLAG_STRIDE = 32;               // one 128-B line per chunk flag
-constexpr unsigned FIN_SPIN_LIMIT = 1u << 22;     // polls ~1 us apart: seconds -- a wait that long is a bug
-
-STF_DEV unsigned load_coh_u(const unsigned* p) {
-  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-STF_DEV void store_coh_u(unsigned* p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// flags: this group's [nch][FIN_FLAG_STRIDE]; err: the slab's sticky timeout word
-template <class Chunk>
-STF_DEV void fin_prologue(unsigned* flags, unsigned* err, const unsigned* epoch, int C, Chunk&& chunk) {
-  const unsigned ep = load_coh_u(epoch);
-  const int nch = (C + 15) / 16;
-  for (int k = blockIdx.x; k < nch; k += gridDim.x) {
-    chunk(k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's device-coherent stores are done
-    __syncthreads();                                   // (and the fold's LDS is free for the next chunk)
-    if (threadIdx.x == 0) store_coh_u(flags + k * FIN_FLAG_STRIDE, ep);
-  }
-  if (threadIdx.x < 64) {                // wave 0 polls the group's flags, one per lane, in parallel
-    unsigned spins = 0;                   // (walking them one by one from one lane measured slower)
-    for (;;) {
-      bool mine = true;
-      for (int t = threadIdx.x; t < nch; t += 64) mine = mine && load_coh_u(flags + t * FIN_FLAG_STRIDE) == ep;
-      if (__all(mine)) break;
-      __builtin_amdgcn_s_sleep(32);
-      if (++spins > FIN_SPIN_LIMIT) {
-        if (threadIdx.x == 0) store_coh_u(err, 1u);
-        break;
-      }
-    }
-  }
-  __syncthreads();                       // (the published values are then read device-coherent)
-}
-
-STF_DEV int fin_nch(int C) { return (C + 15) / 16; }
-
-STF_DEV void fin_fwd(const FinFwd& f, int g) {
-  __shared__ double red[2 * 16 * 16];
-  float* base = f.stats + (size_t)g * f.T * 2 * f.C;
-  const int nch = fin_nch(f.C);
-  fin_prologue(f.flags + (size_t)g * nch * FIN_FLAG_STRIDE, f.flags + (size_t)gridDim.y * nch * FIN_FLAG_STRIDE,
-               f.epoch, f.C, [&](int k) {
-    const int c = k * 16 + (threadIdx.x & 15);
-    const bool cok = c < f.C;
-    double s1, s2;
-    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
-    if (cok && threadIdx.x < 16)
-      bn_fin_fwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.beta, f.mom, f.eps, f.rm, f.rv,
-                           f.mean, f.invstd, f.scale, f.shift);
-  });
-}
-
-STF_DEV void fin_bwd(const FinBwd& f, int g) {
-  __shared__ double red[2 * 16 * 16];
-  float* base = f.partial + (size_t)g * f.T * 2 * f.C;
-  const int nch = fin_nch(f.C);
-  fin_prologue(f.flags + (size_t)g * nch * FIN_FLAG_STRIDE, f.flags + (size_t)gridDim.y * nch * FIN_FLAG_STRIDE,
-               f.epoch, f.C, [&](int k) {
-    const int c = k * 16 + (threadIdx.x & 15);
-    const bool cok = c < f.C;
-    double s1, s2;
-    stf::fold16_pair_256(base, f.S, 2L * f.C, f.C, c, cok, red, s1, s2);
-    if (cok && threadIdx.x < 16)
-      bn_fin_bwd_out<true>(base, g, c, gridDim.y, f.C, f.Mg, s1, s2, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta,
-                           f.coef);
-  });
-}
-
-__global__ void fin_epoch_bump_kernel(unsigned* epoch) {
-  if (threadIdx.x == 0) epoch[0] = epoch[0] + 1u;
-}
-
 // ------------------------------------------------------------------ apply
 // res_mode 0: none, 1: + res tensor, 2: + (res*rscale[g] + rshift[g])
-// FIN (one statistics group): scale/shift are written by this launch (fin_fwd) before they are read
-template <bool POOL, bool FIN>
+template <bool POOL>
 __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, int H, int W, int C, long Mg,
                               const float* scale, const float* shift, int relu, int res_mode,
                               const uint16_t* __restrict__ res, int rcs, const float* __restrict__ rscale,
                               const float* __restrict__ rshift, uint16_t* __restrict__ out, int ocs,
-                              uint16_t* __restrict__ pooled, FinFwd fin) {
+                              uint16_t* __restrict__ pooled) {
   const int CG = C / 8;
-  // FIN (launched with one group only): a thread's channel chunk is fixed (the grid stride is a
-  // multiple of C / 8), so its affine is read once, device-coherent, after the finalize
-  float fsc[8], fsh[8];
-  if (FIN) {
-    fin_fwd(fin, 0);
-    const int cg0 = (int)((blockIdx.x * (long)NT + threadIdx.x) % CG);
-    load_affine_coh(scale, cg0 * 8, fsc);
-    load_affine_coh(shift, cg0 * 8, fsh);
-  }
   const long units = POOL ? N * (H / 2) * (W / 2) * CG : N * H * W * CG;
   for (long u = blockIdx.x * (long)NT + threadIdx.x; u < units; u += (long)gridDim.x * NT) {
     const int cg = (int)(u % CG);
@@ -290,13 +149,8 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
     if (!POOL) {
       const int g = (int)(pix / Mg);
       float sc[8], sh[8], v[8];
-      if (FIN) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { sc[j] = fsc[j]; sh[j] = fsh[j]; }
-      } else {
-        load_affine(scale + (size_t)g * C, cg * 8, sc);
-        load_affine(shift + (size_t)g * C, cg * 8, sh);
-      }
+      load_affine(scale + (size_t)g * C, cg * 8, sc);
+      load_affine(shift + (size_t)g * C, cg * 8, sh);
       unpack8(*reinterpret_cast<const uint4*>(y + pix * ycs + cg * 8), v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
@@ -325,13 +179,8 @@ __global__ void bn_act_kernel(const uint16_t* __restrict__ y, int ycs, long N, i
       const int py = rem / Wp, px = rem - py * Wp;
       const int g = (int)(n * H * W / Mg);
       float sc[8], sh[8], mx[8];
-      if (FIN) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { sc[j] = fsc[j]; sh[j] = fsh[j]; }
-      } else {
-        load_affine(scale + (size_t)g * C, cg * 8, sc);
-        load_affine(shift + (size_t)g * C, cg * 8, sh);
-      }
+      load_affine(scale + (size_t)g * C, cg * 8, sc);
+      load_affine(shift + (size_t)g * C, cg * 8, sh);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const long p = (n * H + 2 * py + (d >> 1)) * W + 2 * px + (d & 1);
@@ -576,7 +425,7 @@ __global__ __launch_bounds__(stf::FOLD_NT) void bn_bwd_finalize_kernel(float* __
   float* base = partial + (size_t)g * T * 2 * C;
   double s1, s2;
   stf::fold16_pair(base, S, 2L * C, C, c, cok, red, s1, s2);
-  if (lead) bn_fin_bwd_out<false>(base, g, c, G, C, Mg, s1, s2, gamma, mean, invstd, dgamma, dbeta, coef);
+  if (lead) bn_fin_bwd_out(base, g, c, G, C, Mg, s1, s2, gamma, mean, invstd, dgamma, dbeta, coef);
 }
 
 // Deferred running-statistics updates of many grouped BatchNorms in one launch
@@ -691,22 +540,20 @@ __global__ void bn_bwd_apply_kernel(const uint16_t* g, int gcs, const uint16_t* 
 // (checked by the launchers).  Unit u of group g: pixel g * Mg + (u >> cgs), chunk u & (CG - 1).
 constexpr int UPT = 4;
 
-// FIN: scale/shift are written by this launch (fin_fwd) before they are read
-template <bool RES, bool FIN>
+template <bool RES>
 __global__ __launch_bounds__(NT) void bn_act_g_kernel(const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
                                                       const float* scale, const float* shift, int relu,
                                                       int res_mode, const uint16_t* __restrict__ res, int rcs,
                                                       const float* __restrict__ rscale,
                                                       const float* __restrict__ rshift, uint16_t* __restrict__ out,
-                                                      int ocs, FinFwd fin) {
+                                                      int ocs) {
   const int g = blockIdx.y, C = 8 << cgs;
-  if (FIN) fin_fwd(fin, g);
   const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & ((1 << cgs) - 1);
   float sc[8], sh[8], rs[8], rh[8];
-  load_aff<FIN>(scale + (size_t)g * C, cg * 8, sc);
-  load_aff<FIN>(shift + (size_t)g * C, cg * 8, sh);
+  load_affine(scale + (size_t)g * C, cg * 8, sc);
+  load_affine(shift + (size_t)g * C, cg * 8, sh);
   if (RES && res_mode == 2) {
     load_affine(rscale + (size_t)g * C, cg * 8, rs);
     load_affine(rshift + (size_t)g * C, cg * 8, rh);
@@ -821,23 +668,21 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_g_kernel(const uint16_t* __r
 }
 
 // dy = A*g' + B*y + C (as bn_bwd_apply_kernel); bias_partial rows = g * gridDim.x + blockIdx.x
-// FIN: coef is written by this launch (fin_bwd) before it is read
-template <bool MASK, bool FIN>
+template <bool MASK>
 __global__ __launch_bounds__(NT) void bn_bwd_apply_g_kernel(const uint16_t* g_in, int gcs,
                                                             const uint16_t* __restrict__ y, int ycs, int Mg, int cgs,
                                                             const float* coef, const float* __restrict__ mscale,
                                                             const float* __restrict__ mshift, uint16_t* dy,
-                                                            int dycs, float* __restrict__ bias_partial, FinBwd fin) {
+                                                            int dycs, float* __restrict__ bias_partial) {
   __shared__ float red[NT][9];
   const int g = blockIdx.y, CG = 1 << cgs, C = 8 << cgs;
-  if (FIN) fin_bwd(fin, g);
   const int upg = Mg << cgs, S = gridDim.x * NT * UPT;
   const int u0 = blockIdx.x * NT * UPT + threadIdx.x;
   const int cg = threadIdx.x & (CG - 1);
   float A[8], B[8], Cc[8], ms[8], mh[8];
-  load_aff<FIN>(coef + (size_t)g * 3 * C, cg * 8, A);
-  load_aff<FIN>(coef + (size_t)g * 3 * C + C, cg * 8, B);
-  load_aff<FIN>(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
+  load_affine(coef + (size_t)g * 3 * C, cg * 8, A);
+  load_affine(coef + (size_t)g * 3 * C + C, cg * 8, B);
+  load_affine(coef + (size_t)g * 3 * C + 2 * C, cg * 8, Cc);
   if (MASK) {
     load_affine(mscale + (size_t)g * C, cg * 8, ms);
     load_affine(mshift + (size_t)g * C, cg * 8, mh);
@@ -1088,25 +933,24 @@ extern "C" int stf_bn_act(const void* y, int y_cstride, int N, int H, int W, int
     const int cgs = log2i(C / 8);
     const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
     if (res)
-      hipLaunchKernelGGL((bn_act_g_kernel<true, false>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+      hipLaunchKernelGGL((bn_act_g_kernel<true>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
                          (int)Mg, cgs, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
-                         res_shift, (uint16_t*)out, out_cstride, FinFwd{});
+                         res_shift, (uint16_t*)out, out_cstride);
     else
-      hipLaunchKernelGGL((bn_act_g_kernel<false, false>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+      hipLaunchKernelGGL((bn_act_g_kernel<false>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
                          (int)Mg, cgs, scale, shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
-                         (const float*)nullptr, (uint16_t*)out, out_cstride, FinFwd{});
+                         (const float*)nullptr, (uint16_t*)out, out_cstride);
     STF_CHECK_LAUNCH();
     return 0;
   }
   if (pooled)
-    hipLaunchKernelGGL((bn_act_kernel<true, false>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+    hipLaunchKernelGGL((bn_act_kernel<true>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
                        (long)N, H, W, C, Mg, scale, shift, relu, 0, (const uint16_t*)nullptr, 0,
-                       (const float*)nullptr, (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled,
-                       FinFwd{});
+                       (const float*)nullptr, (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled);
   else
-    hipLaunchKernelGGL((bn_act_kernel<false, false>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
+    hipLaunchKernelGGL((bn_act_kernel<false>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
                        (long)N, H, W, C, Mg, scale, shift, relu, res_mode, (const uint16_t*)res, res_cstride,
-                       res_scale, res_shift, (uint16_t*)out, out_cstride, (uint16_t*)nullptr, FinFwd{});
+                       res_scale, res_shift, (uint16_t*)out, out_cstride, (uint16_t*)nullptr);
   STF_CHECK_LAUNCH();
   return 0;
 }
@@ -1228,13 +1072,13 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
     const dim3 grid(tpg, groups);
     const int cgs = log2i(C / 8);
     if (mask_scale)
-      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<true, false>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<true>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
                          (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
-                         dy_cstride, bias_partial, FinBwd{});
+                         dy_cstride, bias_partial);
     else
-      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<false, false>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
+      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<false>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
                          (const uint16_t*)y, y_cstride, (int)Mg, cgs, coef, mask_scale, mask_shift, (uint16_t*)dy,
-                         dy_cstride, bias_partial, FinBwd{});
+                         dy_cstride, bias_partial);
     tiles = tpg * groups;
   } else {
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(tiles), dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
@@ -1247,92 +1091,6 @@ extern "C" int stf_bn_bwd_apply(const void* g, int g_cstride, const void* y, int
     hipLaunchKernelGGL(stf_tile_sum_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, s, bias_partial, S, C, dbias);
     STF_CHECK_LAUNCH();
   }
-  return 0;
-}
-
-// ---- finalize fused into its consumer (include/stfunet.h, ABI v13)
-extern "C" int stf_bn_fin_ok(int64_t M, int C, int groups) {
-  return groups >= 1 && C % 8 == 0 && M % groups == 0 && bn_g_ok(M / groups, C) ? 1 : 0;
-}
-
-extern "C" int stf_bn_fin_flags_words(int C, int groups) { return groups * ((C + 15) / 16) * FIN_FLAG_STRIDE + 1; }
-
-extern "C" int stf_bn_fin_epoch_bump(unsigned* epoch, stf_stream_t stream) {
-  if (!epoch) return STF_EINVAL;
-  hipLaunchKernelGGL(fin_epoch_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, epoch);
-  STF_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int stf_bn_act_fin(const stf_bn_fin* f, const void* y, int y_cstride, int N, int H, int W, int relu,
-                              const void* res, int res_cstride, const float* res_scale, const float* res_shift,
-                              void* out, int out_cstride, void* pooled, stf_stream_t stream) {
-  if (!f || !f->stats || !f->flags || !f->epoch || !f->gamma || !f->beta || !f->mean || !f->invstd || !f->scale ||
-      !f->shift)
-    return STF_EINVAL;
-  const int C = f->C, groups = f->groups;
-  const long M = (long)N * H * W;
-  if (f->M != M || f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || N % groups || y_cstride % 8 || out_cstride % 8)
-    return STF_EINVAL;
-  if (res && (res_cstride % 8 || pooled)) return STF_EINVAL;
-  if (pooled && (((H | W) & 1) || groups != 1)) return STF_EINVAL;   // pooled: one statistics group
-  if (groups > 1 && f->running_mean) return STF_EINVAL;   // grouped running stats: parked (stf_bn_running_batch)
-  hipStream_t s = (hipStream_t)stream;
-  const long Mg = M / groups;
-  const int S = stf::colsum_stage1(f->stats, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
-  const FinFwd fin{f->stats, S, f->tiles, C, Mg, f->gamma, f->beta, f->momentum, f->eps, f->running_mean,
-                   f->running_var, f->mean, f->invstd, f->scale, f->shift, f->flags, f->epoch};
-  if (pooled) {
-    const long units = (long)N * (H / 2) * (W / 2) * (C / 8);
-    const long blocks = std::min<long>((units + NT - 1) / NT, 8192);
-    hipLaunchKernelGGL((bn_act_kernel<true, true>), dim3(blocks), dim3(NT), 0, s, (const uint16_t*)y, y_cstride,
-                       (long)N, H, W, C, Mg, f->scale, f->shift, relu, 0, (const uint16_t*)nullptr, 0,
-                       (const float*)nullptr, (const float*)nullptr, (uint16_t*)out, out_cstride, (uint16_t*)pooled,
-                       fin);
-    STF_CHECK_LAUNCH();
-    return 0;
-  }
-  const int cgs = log2i(C / 8);
-  const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
-  const int res_mode = res ? (res_scale ? 2 : 1) : 0;
-  if (res)
-    hipLaunchKernelGGL((bn_act_g_kernel<true, true>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg,
-                       cgs, f->scale, f->shift, relu, res_mode, (const uint16_t*)res, res_cstride, res_scale,
-                       res_shift, (uint16_t*)out, out_cstride, fin);
-  else
-    hipLaunchKernelGGL((bn_act_g_kernel<false, true>), grid, dim3(NT), 0, s, (const uint16_t*)y, y_cstride, (int)Mg,
-                       cgs, f->scale, f->shift, relu, 0, (const uint16_t*)nullptr, 0, (const float*)nullptr,
-                       (const float*)nullptr, (uint16_t*)out, out_cstride, fin);
-  STF_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int stf_bn_bwd_apply_fin(const stf_bn_bwd_fin* f, const void* g, int g_cstride, const void* y,
-                                    int y_cstride, const float* mask_scale, const float* mask_shift, void* dy,
-                                    int dy_cstride, stf_stream_t stream) {
-  if (!f || !f->partial || !f->flags || !f->epoch || !f->gamma || !f->mean || !f->invstd || !f->coef) return STF_EINVAL;
-  const int C = f->C, groups = f->groups;
-  const long M = f->M;
-  if (f->tiles < 1 || !stf_bn_fin_ok(M, C, groups) || y_cstride % 8 || dy_cstride % 8 || g_cstride % 8)
-    return STF_EINVAL;
-  if ((mask_scale == nullptr) != (mask_shift == nullptr)) return STF_EINVAL;
-  if (groups > 1 && (f->dgamma || f->dbeta)) return STF_EINVAL;  // grouped: parked (stf_bn_groupsum_batch)
-  hipStream_t s = (hipStream_t)stream;
-  const long Mg = M / groups;
-  const int S = stf::colsum_stage1(f->partial, f->tiles, 2L * C, s, groups, stf::FOLD16_ROWS);
-  const FinBwd fin{f->partial, S, f->tiles, C, Mg, f->gamma, f->mean, f->invstd, f->dgamma, f->dbeta, f->coef,
-                   f->flags, f->epoch};
-  const int cgs = log2i(C / 8);
-  const dim3 grid(g_tiles(Mg * (C / 8), groups, 8192), groups);
-  if (mask_scale)
-    hipLaunchKernelGGL((bn_bwd_apply_g_kernel<true, true>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
-                       (const uint16_t*)y, y_cstride, (int)Mg, cgs, f->coef, mask_scale, mask_shift, (uint16_t*)dy,
-                       dy_cstride, (float*)nullptr, fin);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_g_kernel<false, true>), grid, dim3(NT), 0, s, (const uint16_t*)g, g_cstride,
-                       (const uint16_t*)y, y_cstride, (int)Mg, cgs, f->coef, mask_scale, mask_shift, (uint16_t*)dy,
-                       dy_cstride, (float*)nullptr, fin);
-  STF_CHECK_LAUNCH();
   return 0;
 }
 

@@ -43,6 +43,11 @@ struct Geo {
   // halo kernel: keep a ring stage's weight rows across items when they are the rows
   // the next fill needs (same 64-channel output slice and source chunk)
   int wkeep;
+  // halo kernel launch knobs: xcd = XCD-aware item ranges (the blocks that share an XCD walk
+  // one contiguous run of items: same output slice -> its weight rows stay in that XCD's L2);
+  // stag = which wave half issues its DMA share at tap 4 (0: odd waves, 1: waves >= NW/2 --
+  // the SIMD partners); prio = s_setprio(1) for waves >= NW/2
+  int xcd, stag, prio;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -953,15 +958,25 @@ STF_DEV int halo_pixel(int p, int img, int ty, int tx, int Hd, int Wd) {
 // small image fills the wide tile instead of half a 16 x 16 one: twice the pixels per stage
 // for the same weight rows.  Neighbouring images share one zero column in the halo (image
 // b's column x sits at halo column b * (IW + 1) + 1 + x), PW + IX + 1 columns in all.
-template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT, bool BNR, int IX>
+// DEFER (8-wave, 2-stage direct epilogues): the second wave half (waves NW/2.., the SIMD
+// partners of the first half) runs each item's epilogue after the next stage barrier, ahead of
+// its next taps, so on every SIMD one wave's epilogue (VALU, stores) overlaps its partner's
+// MFMAs instead of both idling the matrix pipe together; BatchNorm partials are then kept per
+// wave (one statistics row per (group, workgroup, wave): no cross-wave LDS pass, no epilogue
+// barrier) and the BN-backward y tile is loaded to registers.
+template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT, bool BNR, int IX, bool DEFER_T = false>
 __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int TX, int per, int rem) {
   constexpr int NTH = 64 * NW, BN = 64, RPI = 16;       // 64-B rows: 16 per 1-KiB DMA instruction
   constexpr int IW = PW / IX;                           // image width in a multi-image tile
   constexpr int HW = PW + IX + 1, HR = (PH + 2) * HW;   // halo rows
-  constexpr int HI = (HR + RPI * NW - 1) / (RPI * NW);  // halo DMA instructions per wave
-  constexpr int WI = (9 * BN + RPI * NW - 1) / (RPI * NW);
-  constexpr int HROWS = HI * RPI * NW, WROWS = WI * RPI * NW;
+  // DMA instructions per stage, dealt to the waves as evenly as they go (wave w: hcnt(w) from
+  // hbeg(w)); the ring holds exactly these rows, so the stages leave room for the affine area
+  constexpr int HIN = (HR + RPI - 1) / RPI, WIN = 9 * BN / RPI;
+  constexpr int HI = (HIN + NW - 1) / NW, WI = (WIN + NW - 1) / NW;   // per wave, at most
+  constexpr int HROWS = HIN * RPI, WROWS = WIN * RPI;
   constexpr int STAGE = (HROWS + WROWS) * 64;
+  constexpr int AFF = STAGES * STAGE;                 // BNR: per-wave BN affine [4][64] fp32 after the ring
+  static_assert(9 * BN % RPI == 0, "weight rows");
   constexpr int PX = PH * PW, WTM = PX / NW, TM = WTM / 16, TN = BN / 16;
   constexpr int PPP = NTH / 8, NSTORE = PX / PPP;      // epilogue: pixels per pass, stores per lane
   // next stage's DMA (STAGES == 2): even waves at the stage start, odd waves after tap 4.
@@ -971,19 +986,32 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   // instructions over the taps only moves the stall into the taps: the DMA path itself
   // is the limit, fewer bytes per FLOP is what would help.
   constexpr bool STAGGER = STAGES == 2 && NW == 8;
+  constexpr bool DF = DEFER_T && DIRECT != 0 && STAGGER;   // the deferred epilogue (8-wave direct kernels)
   static_assert((WTM == 64 || WTM == 32) && PW % 16 == 0 && PX % PPP == 0, "tile");
-  static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE && NW * 3 * 64 * 4 * 2 + PX * 128 <= STAGE, "epilogue scratch");
-  static_assert(STAGES * STAGE * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  static_assert(PX * 128 + NW * 2 * 64 * 4 <= STAGE, "epilogue scratch");
+  // per-wave epilogue scratch after the ring (BNR or DF): [scale | shift | mean | invstd][64] fp32 of
+  // the current (group, slice) for the BN-backward reduction, or (DF forward) the slice's 64 biases
+  constexpr int EPS = (BNR || DF) ? NW * 1024 : 0;
+  static_assert((AFF + EPS) * (STAGES == 1 ? 2 : 1) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE + EPS];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar DMA addressing
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
+  const bool late = (DF || a.stag) ? wave >= NW / 2 : (wave & 1);   // issues its DMA share at tap 4
+  if (a.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
   const int ntiles = (a.N / IX) * tpi;                  // items: channel slice major, pixel tile minor
   const int ipg = a.Mg / (a.Hd * a.Wd);                 // images per statistics group
-  const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
-  const int it0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  // virtual block id: a bijection of blockIdx.x; every per-block quantity (item range,
+  // statistics row) is keyed by it, so the outputs do not depend on the mapping
+  int vb = blockIdx.x;
+  if (a.xcd && gridDim.x > 8) {
+    const int G = gridDim.x, x = vb & 7, k = vb >> 3, q = G >> 3, r = G & 7;
+    vb = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+  }
+  const int cnt = per + (int)(vb < rem);
+  const int it0 = vb * per + min(vb, rem);
   const int S = cnt * CC;
   if (S == 0) return;
 
@@ -1007,10 +1035,12 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
     char* st = smem + buf * STAGE;
+    const int hcnt = HIN / NW + (wave < HIN % NW), hbeg = wave * (HIN / NW) + min(wave, HIN % NW);
+    const int wcnt = WIN / NW + (wave < WIN % NW), wbeg = wave * (WIN / NW) + min(wave, WIN % NW);
 #pragma unroll
     for (int i = 0; i < HI; ++i) {
-      if (i < k0 || i >= k1) continue;
-      const int hr = (wave * HI + i) * RPI + sub;
+      if (i < k0 || i >= k1 || i >= hcnt) continue;
+      const int hr = (hbeg + i) * RPI + sub;
       const int hy = hr / HW, hx = hr - hy * HW;
       int ys = y0 + hy, xs = x0 + hx, im = img;
       if constexpr (IX > 1) {                         // image b, column hx - b (IW + 1) - 1 (-1: a pad)
@@ -1022,12 +1052,12 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       const uint32_t off =
           ok ? (uint32_t)((((im * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hx, slot) * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_src, (__attribute__((address_space(3))) void*)(st + (wave * HI + i) * RPI * 64), 16, off, 0, 0, 0);
+          rs_src, (__attribute__((address_space(3))) void*)(st + (hbeg + i) * RPI * 64), 16, off, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
-      if (HI + i < k0 || HI + i >= k1 || !wload) continue;
-      const int wr = (wave * WI + i) * RPI + sub;       // weight row = tap * 64 + n
+      if (HI + i < k0 || HI + i >= k1 || !wload || i >= wcnt) continue;
+      const int wr = (wbeg + i) * RPI + sub;            // weight row = tap * 64 + n
       const int wrow = wr & 63;
       const int tap = wr >> 6,
                 n = nt * BN + (DIRECT ? ((wrow >> 5) * 32 + ((wrow >> 2) & 3) * 8 + ((wrow >> 4) & 1) * 4 + (wrow & 3))
@@ -1035,7 +1065,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       const bool ok = live && wr < 9 * BN;
       const uint32_t off = ok ? (uint32_t)(((size_t)n * a.K + tap * a.Cs + cc * 32 + swzh(wr, slot) * 8) * 2) : BAD;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs_wgt, (__attribute__((address_space(3))) void*)(st + (HROWS + (wave * WI + i) * RPI) * 64), 16, off, 0,
+          rs_wgt, (__attribute__((address_space(3))) void*)(st + (HROWS + (wbeg + i) * RPI) * 64), 16, off, 0,
           0, 0);
     }
   };
@@ -1075,25 +1105,44 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   int iit = it0, icc = 0;                               // issue cursor (last issued stage)
   int cit = it0, ccc = 0;                               // compute cursor
   // BN partial statistics, one row per (group, workgroup): stats [groups][gridDim][2][Nout].
-  // Thread tid < 128 owns (sum | sum of squares, channel col) of the current (group, slice)
-  // and zeroes its rows first (same thread, same addresses: ordered).
+  // Thread tid < 128 owns (sum | sum of squares, channel col) of the current (group, slice) and
+  // zeroes its rows first (same thread, same addresses: ordered).  DF: the two wave halves finish
+  // an item on opposite sides of a barrier, so there is no per-item cross-wave pass: every lane
+  // keeps its wave's running partials of the last KMAX (group, slice) keys in registers (lane (fr,
+  // fk), fragment half h: row half fr >> 3, channel h*32 + fk*8 + (fr & 7), where
+  // row16_reduce_scatter leaves them; the host checks a workgroup's item run spans <= KMAX keys)
+  // and the waves' partials are folded once, in wave order, after the loop.
+  constexpr int KMAX = 2;
   const int q_st = tid >> 6, col_st = tid & 63;
   const int groups = a.M / a.Mg;
   int run_key = -1;
   float run = 0.f;
+  float kr[KMAX][2];                                     // DF: running partials, newest key first
+  int kv[KMAX], nk = 0;                                  // DF: their keys (wave-uniform)
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) { kr[k][0] = kr[k][1] = 0.f; kv[k] = -1; }
   // BNR: the same rows hold the fused BN-backward partials (sum g, sum g*xhat)
   float* const sbuf = BNR ? a.bnr_part : (DIRECT == 1 ? nullptr : a.stats);
+  auto srow = [&](int g) { return (size_t)(g * gridDim.x + vb); };
   auto flush = [&]() {
     const int g = run_key / NTn, nt = run_key - g * NTn;
-    sbuf[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = run;
+    sbuf[(srow(g) * 2 + q_st) * a.Nout + nt * BN + col_st] = run;
   };
   if (sbuf && tid < 128) {
     for (int g = 0; g < groups; ++g)
-      for (int nt = 0; nt < NTn; ++nt)
-        sbuf[((size_t)(g * gridDim.x + blockIdx.x) * 2 + q_st) * a.Nout + nt * BN + col_st] = 0.f;
+      for (int nt = 0; nt < NTn; ++nt) sbuf[(srow(g) * 2 + q_st) * a.Nout + nt * BN + col_st] = 0.f;
   }
+  // BNR: this wave's copy of the BatchNorm affine of the current (group, slice) in LDS,
+  // [scale | shift | mean | invstd][64 channels], reloaded when the key changes
+  float* const aff = reinterpret_cast<float*>(smem + AFF) + wave * 256;
+  int aff_key = -1, bias_key = -1;
   bool epi = false;                                      // previous stage ended with an epilogue (8 stores)
   bool wl_next = true;                                   // the next fill streams weight rows too
+  bool pend = false;                                     // DF: this wave owes item pend_it's epilogue
+  int pend_it = 0;
+  f32x4 bv[TN];                                          // bias of the lane's 16 accumulator channels
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // DIAG 4: per-wave cycle buckets (s_memtime) -- DMA wait, barrier, DMA issue, taps, epilogue
   uint64_t tb[5] = {0, 0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
@@ -1103,14 +1152,225 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       tprev = t;
     }
   };
-  for (int s = 0; s < S; ++s) {
+
+  // ---- direct epilogue of item `item` from acc / bv: lane (fr, fk) holds pixel p's channels
+  // 8fk..8fk+7 (fragments 0,1) and 32+8fk.. (2,3).  Order: pack the accumulators (64 fp32 -> 32
+  // bf16x2 registers, the accumulators die), [BNR: the y tile], the dz stores, then the partial
+  // sums from the packed (stored, rounded) values.  Every load precedes every store (vmcnt
+  // retires in order: a later load would wait for the stores in front of it); invalid pixels get
+  // an out-of-range offset, so every lane issues exactly NSTORE = 2 * TM stores.  Sums: DPP
+  // reduce-scatter over the 16 pixels of a fragment row; without DF one LDS pass over the
+  // waves (the stage just read is the scratch: `buf`).
+  auto direct_epi = [&](int item, int buf) {
+    const int nt = item / ntiles, tile = item - nt * ntiles;
+    const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
+    const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
+    const __amdgpu_buffer_rsrc_t rs_dst = __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    uint4 uq[2][TM];
+    int mq[TM];
+    // bias of the lane's 16 accumulator channels: DF -- from the wave's LDS copy of the slice's
+    // biases (no registers held across the stage), else the registers load_bias filled
+    f32x4 be[TN];
+    if constexpr (DF) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) be[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!BNR && a.bias) {
+        if (nt != bias_key) {                          // same-wave LDS write -> read: ordered
+          bias_key = nt;
+          aff[lane] = a.bias[nt * BN + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) be[j] = *reinterpret_cast<const f32x4*>(aff + (j >> 1) * 32 + fk * 8 + (j & 1) * 4);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) be[j] = bv[j];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int p = wave * WTM + i * 16 + fr;
+      mq[i] = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = acc[i][2 * h][r] + be[2 * h][r];
+          f[4 + r] = acc[i][2 * h + 1][r] + be[2 * h + 1][r];
+        }
+        if (a.accumulate && mq[i] >= 0) {
+          float o[8];
+          unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8), o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += o[e];
+        }
+        uq[h][i] = pack8(f);
+        acc[i][2 * h] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[i][2 * h + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    const int key = (img / ipg) * NTn + nt;
+    float* red = reinterpret_cast<float*>(smem + buf * STAGE);   // [NW][2][64]
+    // BNR scratch without DF: y rows [WTM][128 B] per wave in the stage just read, after the
+    // [NW][2][64] reduction rows (16-B chunk c of pixel row r at slot c ^ (r & 7): conflict-free)
+    char* yl = smem + buf * STAGE + NW * 2 * 64 * 4 + wave * WTM * 128;
+    uint4 yq[2][TM];
+    if constexpr (BNR) {
+      if (key != aff_key) {                             // this wave's affine of (group, slice)
+        aff_key = key;
+        const size_t o = (size_t)(img / ipg) * a.Nout + nt * BN + lane;
+        const float v0 = a.bnr_scale[o], v1 = a.bnr_shift[o], v2 = a.bnr_mean[o], v3 = a.bnr_invstd[o];
+        aff[lane] = v0; aff[64 + lane] = v1; aff[128 + lane] = v2; aff[192 + lane] = v3;
+      }
+      const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)a.bnr_y, 0, (uint32_t)((size_t)a.M * a.bnr_ycs * 2), 0x00020000);
+      if constexpr (DF) {
+        // y straight to registers (the accumulators are dead): lane (fr, fk) loads exactly the
+        // 8 channels of pixel i*16+fr that it holds in uq[h][i]
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const uint32_t off =
+                mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.bnr_ycs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_y, off, 0, 0);
+            yq[h][i] = make_uint4(v.x, v.y, v.z, v.w);
+          }
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
+        (buf ? wkey1 : wkey0) = -1;                     // the y rows overwrite its weight rows
+#pragma unroll
+        for (int k = 0; k < WTM / 8; ++k) {
+          const int r = k * 8 + (lane >> 3), p = wave * WTM + r;       // 8 pixel rows per instruction
+          const int m = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
+          const int c = (lane & 7) ^ (r & 7);
+          const uint32_t off = m >= 0 ? (uint32_t)(((size_t)m * a.bnr_ycs + nt * BN + c * 8) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs_y, (__attribute__((address_space(3))) void*)(yl + k * 1024), 16, off, 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const uint4 u = uq[h][i];
+        const uint32_t off =
+            mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+      }
+    float res[2] = {0.f, 0.f};                           // row16_reduce_scatter results per half
+    if constexpr (BNR) {
+      // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat), like stf_bn_bwd_reduce
+      // the y loads (issued before the stores) have landed; the stores stay in flight
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * TM) : "memory");
+      auto aff8 = [&](int k, int c0, float* v) {
+        const float4 lo = *reinterpret_cast<const float4*>(aff + k * 64 + c0);
+        const float4 hi = *reinterpret_cast<const float4*>(aff + k * 64 + c0 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      };
+      const bool norelu = !a.bnr_relu;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // sum g*y per lane (TM pixels), turned into sum g*xhat = invstd*(sum g*y - mean*sum g)
+        float q1[8], q2[8], sc[8], sh[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { q1[e] = 0.f; q2[e] = 0.f; }
+        aff8(0, h * 32 + fk * 8, sc);
+        aff8(1, h * 32 + fk * 8, sh);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float g[8], yv[8];
+          unpack8(uq[h][i], g);
+          const int r = i * 16 + fr;
+          if constexpr (DF) unpack8(yq[h][i], yv);
+          else unpack8(*reinterpret_cast<const uint4*>(yl + r * 128 + (((h * 4 + fk) ^ (r & 7)) << 4)), yv);
+          const bool valid = mq[i] >= 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            // bitwise, not short-circuit: a select, no branch
+            const bool keep = valid & (norelu | (yv[e] * sc[e] + sh[e] > 0.f));
+            const float gg = keep ? g[e] : 0.f;
+            q1[e] += gg;
+            q2[e] += gg * yv[e];
+          }
+        }
+        float mu[8], is[8], v[16];
+        aff8(2, h * 32 + fk * 8, mu);
+        aff8(3, h * 32 + fk * 8, is);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = q1[e];
+          v[8 + e] = is[e] * (q2[e] - mu[e] * q1[e]);
+        }
+        res[h] = row16_reduce_scatter(v, fr);
+      }
+    } else if constexpr (DIRECT == 2) {
+      // BN statistics (sum, sum of squares) of the stored values
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float g[8];
+          unpack8(uq[h][i], g);
+          const float w = mq[i] >= 0 ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { v[e] += w * g[e]; v[8 + e] += w * g[e] * g[e]; }
+        }
+        // lane fr ends with value fr: sum (fr < 8) or sum of squares of channel fr & 7
+        res[h] = row16_reduce_scatter(v, fr);
+      }
+      if constexpr (!DF) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
+      }
+    }
+    if (sbuf) {
+      if constexpr (DF) {
+        // this wave's running partials of the current (group, slice); a new key shifts them
+        if (nk == 0 || key != kv[0]) {
+#pragma unroll
+          for (int k = KMAX - 1; k > 0; --k) { kr[k][0] = kr[k - 1][0]; kr[k][1] = kr[k - 1][1]; kv[k] = kv[k - 1]; }
+          kr[0][0] = kr[0][1] = 0.f;
+          kv[0] = key;
+          ++nk;
+        }
+        kr[0][0] += res[0];
+        kr[0][1] += res[1];
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = res[h];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (tid < 128) {
+          const int q = tid >> 6, col = tid & 63;
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
+          if (key != run_key) {
+            if (run_key >= 0) flush();
+            run_key = key;
+            run = 0.f;
+          }
+          run += t;
+        }
+      }
+    }
+  };
+
+  // DF: one more pass through the loop head after the last stage runs the last epilogue
+  for (int s = 0; s < S + (DF ? 1 : 0); ++s) {
     const int buf = STAGES == 2 ? (s & 1) : 0;
     stamp(-1);
-    f32x4 bv[TN];
     auto load_bias = [&]() {
       // bias of this lane's 16 accumulator channels, loaded BEFORE the next DMA so
       // that waiting for it never waits for the DMA (BNR: a dgrad, no bias)
-      if constexpr (BNR) {
+      if constexpr (BNR || (DF && DIRECT)) {           // (DF: direct_epi reads them from LDS)
 #pragma unroll
         for (int j = 0; j < TN; ++j) bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
       } else if (ccc == CC - 1) {
@@ -1128,17 +1388,29 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       stamp(0);
       epi = false;
-      __builtin_amdgcn_s_barrier();
+      if constexpr (DF) {
+        // the epilogue of the item that ended with the previous stage: the first wave half runs
+        // it before this stage barrier, the second half (its SIMD partners) after it, ahead of
+        // its taps -- one code site, the barrier instruction placed by wave half (s_barrier
+        // counts arrivals, not program points; `late` is wave-uniform)
+        if (late) __builtin_amdgcn_s_barrier();
+        if (pend) { direct_epi(pend_it, buf ^ 1); pend = false; }
+        if (!late) __builtin_amdgcn_s_barrier();
+        if (s == S) break;
+      } else {
+        __builtin_amdgcn_s_barrier();
+      }
       stamp(1);
       load_bias();
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
       wl_next = need_w(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
-      // even waves issue the next stage's DMA now, odd waves after tap 4: the address
-      // path takes ~300 cycles per 1-KiB LDS-DMA instruction under load, and with all
-      // eight waves issuing at once both waves of a SIMD stalled together (DIAG 4: a third
-      // of the time); staggered, one wave of each SIMD computes while the other issues
-      if (!STAGGER || !(wave & 1)) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1), wl_next);
+      // the first wave half issues the next stage's DMA now, the second (its SIMD partners;
+      // a.stag = 0: the odd waves) after tap 4: the address path takes ~300 cycles per 1-KiB
+      // LDS-DMA instruction under load, and with all eight waves issuing at once both waves of a
+      // SIMD stalled together (DIAG 4: a third of the time); staggered, one wave of each SIMD
+      // computes while the other issues
+      if (!STAGGER || !late) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1), wl_next);
       stamp(2);
     } else {
       // single stage: every wave is done with the buffer, refill it, wait
@@ -1176,7 +1448,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     for (int t = 0; t < 9; ++t) {
       const int b = t & 1;
       if constexpr (STAGGER) {
-        if (t == 4 && (wave & 1)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
+        if (t == 4 && late) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
       }
       if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
       // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
@@ -1204,170 +1476,16 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     }
     stamp(3);
     if (DIRECT && ccc + 1 == CC) {
-      // ---- direct epilogue: lane (fr, fk) holds pixel p's channels 8fk..8fk+7 (fragments
-      // 0,1) and 32+8fk.. (2,3).  Order: pack the accumulators (64 fp32 -> 32 bf16x2
-      // registers, the accumulators die), [BNR: LDS-DMA the y tile], the dz stores, then
-      // the partial sums from the packed (stored, rounded) values.  Every load precedes
-      // every store (vmcnt retires in order: a later load would wait for the stores in
-      // front of it); invalid pixels get an out-of-range offset, so every lane issues
-      // exactly NSTORE = 2 * TM stores.  Sums: DPP reduce-scatter over the 16 pixels of a
-      // fragment row, one LDS pass over the waves.
-      const int nt = cit / ntiles, tile = cit - nt * ntiles;
-      const int tq = tile / tpi, t2 = tile - tq * tpi, ty = t2 / TX, tx = t2 - ty * TX, img = tq * IX;
-      const uint32_t dst_records = (uint32_t)((size_t)a.M * a.dcs * 2);
-      const __amdgpu_buffer_rsrc_t rs_dst =
-          __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, dst_records, 0x00020000);
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      uint4 uq[2][TM];
-      int mq[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int p = wave * WTM + i * 16 + fr;
-        mq[i] = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float f[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            f[r] = acc[i][2 * h][r] + bv[2 * h][r];
-            f[4 + r] = acc[i][2 * h + 1][r] + bv[2 * h + 1][r];
-          }
-          if (a.accumulate && mq[i] >= 0) {
-            float o[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.dst + (size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8), o);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] += o[e];
-          }
-          uq[h][i] = pack8(f);
-          acc[i][2 * h] = f32x4{0.f, 0.f, 0.f, 0.f};
-          acc[i][2 * h + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      float* red = reinterpret_cast<float*>(smem + buf * STAGE);   // [NW][2][64]
-      // BNR scratch in the stage just read: affine [4][64] and y rows [WTM][128 B] per wave
-      // (16-B chunk c of pixel row r at slot c ^ (r & 7): conflict-free reads)
-      float* aff = reinterpret_cast<float*>(smem + buf * STAGE + NW * 2 * 64 * 4) + wave * 256;
-      char* yl = smem + buf * STAGE + NW * 3 * 64 * 4 * 2 + wave * WTM * 128;
-      float aff_pre[4];                                 // BNR: (scale, shift, mean, invstd)[channel lane]
-      if constexpr (BNR) {
-        const size_t o = (size_t)(img / ipg) * a.Nout + nt * BN + lane;
-        aff_pre[0] = a.bnr_scale[o]; aff_pre[1] = a.bnr_shift[o];
-        aff_pre[2] = a.bnr_mean[o]; aff_pre[3] = a.bnr_invstd[o];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
-        (buf ? wkey1 : wkey0) = -1;                     // the y rows overwrite its weight rows
-        const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)a.bnr_y, 0, (uint32_t)((size_t)a.M * a.bnr_ycs * 2), 0x00020000);
-#pragma unroll
-        for (int k = 0; k < WTM / 8; ++k) {
-          const int r = k * 8 + (lane >> 3), p = wave * WTM + r;       // 8 pixel rows per instruction
-          const int m = halo_pixel<PH, PW, IX>(p, img, ty, tx, a.Hd, a.Wd);
-          const int c = (lane & 7) ^ (r & 7);
-          const uint32_t off = m >= 0 ? (uint32_t)(((size_t)m * a.bnr_ycs + nt * BN + c * 8) * 2) : 0xFFFFFFF0u;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs_y, (__attribute__((address_space(3))) void*)(yl + k * 1024), 16, off, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const uint4 u = uq[h][i];
-          const uint32_t off =
-              mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
-        }
-      if constexpr (BNR) {
-        // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat), like stf_bn_bwd_reduce
-#pragma unroll
-        for (int k = 0; k < 4; ++k) aff[k * 64 + lane] = aff_pre[k];   // same-wave LDS ops are ordered
-        // the y DMA (issued before the stores) has landed; the stores stay in flight
-        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * TM) : "memory");
-        auto aff8 = [&](int k, int c0, float* v) {
-          const float4 lo = *reinterpret_cast<const float4*>(aff + k * 64 + c0);
-          const float4 hi = *reinterpret_cast<const float4*>(aff + k * 64 + c0 + 4);
-          v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-        };
-        const bool norelu = !a.bnr_relu;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          // sum g*y per lane (TM pixels), turned into sum g*xhat = invstd*(sum g*y - mean*sum g)
-          float q1[8], q2[8], sc[8], sh[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { q1[e] = 0.f; q2[e] = 0.f; }
-          aff8(0, h * 32 + fk * 8, sc);
-          aff8(1, h * 32 + fk * 8, sh);
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float g[8], yv[8];
-            unpack8(uq[h][i], g);
-            const int r = i * 16 + fr;
-            unpack8(*reinterpret_cast<const uint4*>(yl + r * 128 + (((h * 4 + fk) ^ (r & 7)) << 4)), yv);
-            const bool valid = mq[i] >= 0;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              // bitwise, not short-circuit: a select, no branch
-              const bool keep = valid & (norelu | (yv[e] * sc[e] + sh[e] > 0.f));
-              const float gg = keep ? g[e] : 0.f;
-              q1[e] += gg;
-              q2[e] += gg * yv[e];
-            }
-          }
-          float mu[8], is[8], v[16];
-          aff8(2, h * 32 + fk * 8, mu);
-          aff8(3, h * 32 + fk * 8, is);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[e] = q1[e];
-            v[8 + e] = is[e] * (q2[e] - mu[e] * q1[e]);
-          }
-          red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = row16_reduce_scatter(v, fr);
-        }
-      } else if constexpr (DIRECT == 2) {
-        // BN statistics (sum, sum of squares) of the stored values
-        float s12[2][2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float v[16];
-#pragma unroll
-          for (int e = 0; e < 16; ++e) v[e] = 0.f;
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float g[8];
-            unpack8(uq[h][i], g);
-            const float w = mq[i] >= 0 ? 1.f : 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { v[e] += w * g[e]; v[8 + e] += w * g[e] * g[e]; }
-          }
-          // lane fr ends with value fr: sum (fr < 8) or sum of squares of channel fr & 7
-          s12[h][0] = row16_reduce_scatter(v, fr);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                   // every wave is done reading this stage
-#pragma unroll
-        for (int h = 0; h < 2; ++h) red[(wave * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = s12[h][0];
-      }
-      if (sbuf) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (tid < 128) {
-          const int q = tid >> 6, col = tid & 63;
-          float t = 0.f;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) t += red[(w * 2 + q) * 64 + col];
-          const int key = (img / ipg) * NTn + nt;
-          if (key != run_key) {
-            if (run_key >= 0) flush();
-            run_key = key;
-            run = 0.f;
-          }
-          run += t;
-        }
+      if constexpr (DF) {                              // at the next loop head
+        pend = true;
+        pend_it = cit;
+      } else {
+        direct_epi(cit, buf);
+        epi = true;
       }
       stamp(4);
       ccc = 0;
       ++cit;
-      epi = true;
       continue;
     }
     if constexpr (DIRECT) {                            // (the last chunk took the branch above)
@@ -1469,27 +1587,57 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       epi = true;
     }
   }
-  if (sbuf && tid < 128 && run_key >= 0) flush();
+  if constexpr (DF) {
+    if (sbuf) {
+      // every wave has left the loop (the second half after its last epilogue) and every DMA has
+      // landed (the loop head's vmcnt(0)): the ring is free.  Partials [KMAX][NW][2][64] fp32,
+      // folded in wave order by the threads that own the rows.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      float* part = reinterpret_cast<float*>(smem);
+      const int nkk = nk < KMAX ? nk : KMAX;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < nkk)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            part[((k * NW + wave) * 2 + (fr >> 3)) * 64 + h * 32 + fk * 8 + (fr & 7)] = kr[k][h];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (tid < 128) {
+        for (int k = 0; k < nkk; ++k) {
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += part[((k * NW + w) * 2 + q_st) * 64 + col_st];
+          run_key = kv[k];
+          run = t;
+          flush();
+        }
+      }
+    }
+  } else {
+    if (sbuf && tid < 128 && run_key >= 0) flush();
+  }
   if constexpr (DIAG == 4) {                           // a.stats doubles as the [grid][NW][8] u64 buffer
     if (lane == 0) {
-      unsigned long long* d = reinterpret_cast<unsigned long long*>(a.stats) + (blockIdx.x * NW + wave) * 8;
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(a.stats) + (vb * NW + wave) * 8;
 #pragma unroll
       for (int k = 0; k < 5; ++k) d[k] = tb[k];
     }
   }
 }
 
-template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT = 0, bool BNR = false>
+template <int PH, int PW, int NW, int STAGES, int DIAG, int DIRECT = 0, bool BNR = false, bool DEFER = false>
 __global__ __launch_bounds__(64 * NW, (STAGES == 1) ? 2 : 1) void conv3x3_halo_kernel(Geo a, uint32_t src_bytes,
                                                                                     int TY, int TX, int per, int rem) {
-  halo_body<PH, PW, NW, STAGES, DIAG, DIRECT, BNR, 1>(a, src_bytes, TY, TX, per, rem);
+  halo_body<PH, PW, NW, STAGES, DIAG, DIRECT, BNR, 1, DEFER>(a, src_bytes, TY, TX, per, rem);
 }
 
 // two 16 x 16 images per 16 x 32 tile (IX = 2); TY = TX = 1
-template <int DIRECT, bool BNR>
+template <int DIRECT, bool BNR, bool DEFER = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo2_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
                                                                int rem) {
-  halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2>(a, src_bytes, TY, TX, per, rem);
+  halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2, DEFER>(a, src_bytes, TY, TX, per, rem);
 }
 
 // four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves, one stage, two workgroups
@@ -1716,6 +1864,32 @@ bool halo_direct(const stf_igemm_args* a) {
 bool bnr_fused(const stf_igemm_args* a, char k) {
   static const bool on = [] { const char* e = getenv("STF_BNR_FUSED"); return !(e && e[0] == '0'); }();
   return on && a->bnr && k == 'H' && halo_direct(a) && halo_variant() == 0;
+}
+
+int halo_ix(const stf_igemm_args* a, bool with_stats);
+int halo_grid(const stf_igemm_args* a, int ix);
+void halo_tiles(const stf_conv_geom& c, int& ty, int& tx);
+
+// deferred epilogue of the second wave half (halo_body DEFER; STF_HALO_DEFER=0: off, A/B).  Its
+// statistics fold keeps at most 2 (group, slice) keys per workgroup: the item run of a workgroup
+// (items / grid + 1, slice-major, image-major within a slice) must not span more.
+bool halo_defer(const stf_igemm_args* a) {
+  static const int on = [] { const char* e = getenv("STF_HALO_DEFER"); return e ? atoi(e) : 0; }();
+  if (!(on && halo_direct(a) && halo_variant() == 0 && !halo8(a))) return false;
+  // (not the two-image 16 x 16 tiles: their deferred variants spill registers)
+  const int ix = halo_ix(a, a->stats != nullptr);
+  if (ix > 1) return false;
+  if (!a->stats && !a->bnr) return true;                 // no statistics rows
+  const stf_conv_geom& c = a->g;
+  int ty, tx;
+  halo_tiles(c, ty, tx);
+  if (ix > 1) ty = tx = 1;
+  const long M = (long)c.N * c.Hd * c.Wd;
+  const long Mg = a->group_rows > 0 ? a->group_rows : M;
+  const long run = (Mg / ((long)c.Hd * c.Wd) / ix) * ty * tx;   // items per (group, slice) key
+  const long items = (long)(c.N / ix) * ty * tx * (a->Nout / 64);
+  const long per = items / halo_grid(a, ix) + 1;
+  return run > 0 && (per + run - 1) / run + 1 <= 2;
 }
 
 int num_cus() {
@@ -1995,12 +2169,14 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
       if (halo8(a))
         snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
       else if (halo_ix(a, a->stats != nullptr) > 1)
-        snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
-                 bnr_fused(a, k) ? "true" : "false");
-      else if (halo_variant() == 1) snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false>", HALO_PW);
+        snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
+                 bnr_fused(a, k) ? "true" : "false", halo_defer(a) ? "true" : "false");
+      else if (halo_variant() == 1)
+        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false, false>", HALO_PW);
       else
-        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, %d, %s>", halo_pw(c),
-                 halo_direct(a) ? (a->stats ? 2 : 1) : 0, bnr_fused(a, k) ? "true" : "false");
+        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, %d, %s, %s>", halo_pw(c),
+                 halo_direct(a) ? (a->stats ? 2 : 1) : 0, bnr_fused(a, k) ? "true" : "false",
+                 halo_defer(a) ? "true" : "false");
       break;
     case 'A': snprintf(buf, sizeof buf, "igemm_dma_kernel<128, 128, 2, 2, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
     case 'E': snprintf(buf, sizeof buf, "igemm_dma_kernel<256, 64, 4, 1, 32, 4, %s, %s, %d, false>", tr, sc, epi); break;
@@ -2062,6 +2238,10 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.ksplit = 1; g.ws = nullptr;
   static const int wkeep = [] { const char* e = getenv("STF_HALO_WKEEP"); return e ? atoi(e) : 1; }();
   g.wkeep = wkeep;
+  static const int xcd = [] { const char* e = getenv("STF_HALO_XCD"); return e ? atoi(e) : 0; }();
+  static const int stag = [] { const char* e = getenv("STF_HALO_STAG"); return e ? atoi(e) : 0; }();
+  static const int prio = [] { const char* e = getenv("STF_HALO_PRIO"); return e ? atoi(e) : 0; }();
+  g.xcd = xcd; g.stag = stag; g.prio = prio;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
@@ -2115,10 +2295,19 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   } while (0)
     const int d = halo_direct(a) ? (a->stats ? 2 : 1) : 0;
     const int per = (int)(items / grid), rem = (int)(items % grid);
-#define STF_HL(PWV, D, B) hipLaunchKernelGGL((conv3x3_halo_kernel<16, PWV, 8, 2, 0, D, B>), dim3(grid), dim3(512), 0, \
-                                             s, g, src_bytes, ty, tx, per, rem)
-#define STF_H2(D, B) hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B>), dim3(grid), dim3(512), 0, s, g, src_bytes, \
-                                        ty, tx, per, rem)
+    const bool dfr = halo_defer(a);
+#define STF_HL(PWV, D, B) do {                                                                                      \
+      if (dfr) hipLaunchKernelGGL((conv3x3_halo_kernel<16, PWV, 8, 2, 0, D, B, true>), dim3(grid), dim3(512), 0, s, g, \
+                                  src_bytes, ty, tx, per, rem);                                                        \
+      else hipLaunchKernelGGL((conv3x3_halo_kernel<16, PWV, 8, 2, 0, D, B>), dim3(grid), dim3(512), 0, s, g,          \
+                              src_bytes, ty, tx, per, rem);                                                            \
+    } while (0)
+#define STF_H2(D, B) do {                                                                                           \
+      if (dfr) hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B, true>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty,  \
+                                  tx, per, rem);                                                                       \
+      else hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per,   \
+                              rem);                                                                                    \
+    } while (0)
     if (ix == 4) {
       hipLaunchKernelGGL((conv3x3_halo4_kernel<0>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
     } else if (ix > 1) {
@@ -2158,7 +2347,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     const int bmp = cfg_of(k).bm;
     // accumulating: tap-less classes add nothing, skip them (STF_TRANS_SKIP=0: launch them, A/B)
     static const bool skip_on = [] { const char* e = getenv("STF_TRANS_SKIP"); return !(e && e[0] == '0'); }();
-    const int par = a->accumulate && skip_on ? 2 : 1;
+    // (only when the epilogue adds nothing of its own: no bias, statistics or fused BN reduce)
+    const int par = a->accumulate && skip_on && !a->bias && !a->stats && !a->bnr ? 2 : 1;
     long blocks = 0;
     for (int cl = 0; cl < 4; ++cl) {
       const int ntap = ((c.R - (((cl >> 1) + c.pad) & 1) + 1) >> 1) * ((c.S - (((cl & 1) + c.pad) & 1) + 1) >> 1);

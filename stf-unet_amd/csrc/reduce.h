@@ -116,51 +116,6 @@ STF_DEV void fold16_pair(const float* base, int S, long stride, long off2, long 
 
 constexpr int FOLD_NT = 1024;         // block size of the fold16 consumers (finalize kernels)
 
-// fold16_pair's exact summation order (FOLD_NT threads: 64 row-lanes, 16 waves of 4) on a
-// 256-thread block: thread slot s = tid >> 4 plays wave s, i.e. row-lanes 4s..4s+3 -- each lane's
-// two chains as in fold16_pair, the lanes combined as its two shuffles do, ((v0 + v1) + (v2 + v3)),
-// and the 16 wave totals added in order.  Bit-identical results to a FOLD_NT finalize kernel, so
-// the finalize fused into a 256-thread consumer (bn.hip, *_fin) equals the separate launch.
-// ``red`` holds 2 * 16 * 16 doubles.  Returns the totals on threads 0..15.
-STF_DEV void fold16_pair_256(const float* base, int S, long stride, long off2, long c, bool cok, double* red,
-                             double& o1, double& o2) {
-  constexpr int RL = FOLD_NT / 16;
-  const int s = threadIdx.x >> 4, ch = threadIdx.x & 15;
-  // row-lane r's two chains (fold16_pair's loop) -> (sum of the first array, of the second)
-  auto lane = [&](int r, double& v, double& w) {
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    if (cok) {
-      int t = r;
-      for (; t + RL < S; t += 2 * RL) {
-        const float x0 = base[(long)t * stride + c], y0 = base[(long)t * stride + off2 + c];
-        const float x1 = base[(long)(t + RL) * stride + c], y1 = base[(long)(t + RL) * stride + off2 + c];
-        a0 += x0; b0 += y0; a1 += x1; b1 += y1;
-      }
-      for (; t < S; t += RL) {
-        a0 += base[(long)t * stride + c];
-        b0 += base[(long)t * stride + off2 + c];
-      }
-    }
-    v = a0 + a1;
-    w = b0 + b1;
-  };
-  double v0, w0, v1, w1;
-  lane(4 * s, v0, w0);
-  lane(4 * s + 1, v1, w1);
-  const double p = v0 + v1, pw = w0 + w1;
-  lane(4 * s + 2, v0, w0);
-  lane(4 * s + 3, v1, w1);
-  red[s * 16 + ch] = p + (v0 + v1);
-  red[(16 + s) * 16 + ch] = pw + (w0 + w1);
-  __syncthreads();
-  o1 = o2 = 0.0;
-  if (threadIdx.x < 16)
-    for (int q = 0; q < 16; ++q) {
-      o1 += red[q * 16 + threadIdx.x];
-      o2 += red[(16 + q) * 16 + threadIdx.x];
-    }
-}
-
 constexpr long FOLD16_ROWS = 1024;    // finalize kernels read up to this many rows directly
 
 }  // namespace stf

@@ -283,11 +283,23 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
     }
 
   const int steps = t_end - t_begin;
+  // DIAG 4 (timing only, the slabs are overwritten): per-wave cycle buckets (s_memtime) --
+  // load issue, MFMA steps, LDS store (incl. the wait for the loads), barrier
+  uint64_t tb[4] = {0, 0, 0, 0}, tprev = 0;
+  auto stamp = [&](int k) {
+    if constexpr (DIAG == 4) {
+      const uint64_t tt = __builtin_amdgcn_s_memtime();
+      if (k >= 0) tb[k] += tt - tprev;
+      tprev = tt;
+    }
+  };
   if (steps > 0) { load(t_begin); store(0); }
   __syncthreads();
   for (int it = 0; it < steps; ++it) {
     const int cur = it & 1;
+    stamp(-1);
     if (it + 1 < steps && (DIAG != 1 || it < 1)) load(t_begin + it + 1);
+    stamp(0);
     const uint16_t* sa = smem[cur];
     const uint16_t* sb = sa + A_EL;
     if (DIAG == 2) { if (it + 1 < steps) store(cur ^ 1); __syncthreads(); continue; }
@@ -326,11 +338,23 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
         acc[t][i][0] = mfma16x16x32(af[k2][i], bq[st], acc[t][i][0]);
       __builtin_amdgcn_sched_barrier(0);        // keep the prefetch distance (no re-clustering)
     }
+    stamp(1);
     if (it + 1 < steps) store(cur ^ 1);
+    stamp(2);
     __syncthreads();
+    stamp(3);
   }
 
   const int RSC = 9 * a.Cs;
+  if constexpr (DIAG == 4) {
+    if (lane == 0) {
+      const size_t blk = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(a.ws) + (blk * 4 + wave) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = tb[k];
+    }
+    return;
+  }
   float* out = a.ws + (size_t)(a.one_slab ? 0 : split) * a.Nout * RSC;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -837,6 +861,8 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16 && diag == 3)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 3>), grid, dim3(NT), 0, s, w, ty, tx, nt);
+    else if (pw == 16 && diag == 4)
+      hipLaunchKernelGGL((wgrad3x3_kernel<16, 4>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16)
       hipLaunchKernelGGL((wgrad3x3_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else

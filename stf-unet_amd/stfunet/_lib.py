@@ -82,11 +82,6 @@ _SIGS = {
     "stf_bn_bwd_finalize": (c_int, [P, c_int, c_int, c_int, c_int64, P, P, P, P, P, P, P]),
     "stf_bn_bwd_apply_tiles": (c_int, [c_int64, c_int]),
     "stf_bn_bwd_apply": (c_int, [P, c_int, P, c_int, c_int64, c_int, c_int, P, P, P, P, c_int, P, P, P]),
-    "stf_bn_fin_ok": (c_int, [c_int64, c_int, c_int]),
-    "stf_bn_fin_flags_words": (c_int, [c_int, c_int]),
-    "stf_bn_fin_epoch_bump": (c_int, [P, P]),
-    "stf_bn_act_fin": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P, P]),
-    "stf_bn_bwd_apply_fin": (c_int, [P, P, c_int, P, c_int, P, P, P, c_int, P]),
     "stf_head_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "stf_head_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P, P, P, P, c_int, P, P, P, P, P, P]),
     "stf_head_tiles": (c_int, [c_int, c_int, c_int, c_int]),

@@ -11,6 +11,12 @@ slice is enqueued (RCCL runs it on its own stream after an event wait on the
 compute stream) while the remaining backward kernels keep the GPU busy.
 ``finish()`` reduces the last bucket and makes the compute stream wait.
 
+Gradients written on side streams (the STF program's LSTM backwards and weight-gradient
+stream) reach the hook as ``deps``: the bucket that contains them is launched from a joiner
+stream that waits for the compute stream AND those streams, so the compute stream itself
+never waits for a side stream on the hook's account (the schedule with the hook attached is
+the schedule without it).
+
 Buckets are large and few on purpose: xGMI is point-to-point (7 links per GPU),
 RCCL's ring/tree bandwidth per call grows with message size, and each call costs
 tens of microseconds of launch/sync, so ~25-64 MB buckets (2-5 per UNet step)
@@ -35,15 +41,37 @@ class GradAllReduce:
         self.works = []
         self.launched_from = None       # suffix [launched_from, numel) already enqueued
         self.ready_from = None
+        self.deps = []                  # side streams the next bucket must wait for
+
+    def _joiner(self, dev):
+        j = getattr(self, "_join", None)
+        if j is None or j.device != dev:
+            j = self._join = torch.cuda.Stream(device=dev)
+        return j
 
     def _launch(self, lo, hi):
         if hi <= lo:
             return
         t = self.flat.grad[lo:hi]
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
-        self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t))
+        deps, self.deps = self.deps, []
+        if deps and t.is_cuda:
+            js = self._joiner(t.device)
+            js.wait_stream(torch.cuda.current_stream(t.device))
+            for s in deps:
+                js.wait_stream(s)
+            with torch.cuda.stream(js):
+                w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+        else:
+            w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+        self.works.append((w, t))
 
-    def _ready(self, begin):
+    def _ready(self, begin, deps=()):
+        """Flat-gradient elements [begin, numel) are final once the current stream's work and
+        that of the streams in ``deps`` (enqueued so far) have run."""
+        for s in deps:
+            if all(s is not d for d in self.deps):
+                self.deps.append(s)
         if self.launched_from is None:
             self.launched_from = self.ready_from = self.flat.numel
         self.ready_from = min(self.ready_from, begin)

@@ -335,7 +335,8 @@ def train_one_epoch(model, optimizer, data_loader, device, epoch, num_classes, l
         logger.update(loss=loss.item(), lr=lr)
     # the epoch's last steps: a device-side failure flag (cooperative LSTM hand-off timeout)
     # raises here instead of at the next epoch's first step
-    prog = getattr(model, "_program", None)
+    # (through a DistributedDataParallel-style wrapper's .module as well)
+    prog = getattr(getattr(model, "module", model), "_program", None)
     if prog is not None and hasattr(prog, "check_device_errors"):
         prog.check_device_errors(block=True)
     return logger.meters["loss"].global_avg, lr

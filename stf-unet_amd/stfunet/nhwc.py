@@ -543,62 +543,17 @@ def channel_sum(x: Feat, out):
 
 # ------------------------------------------------------------------ BatchNorm
 class BNState:
-    """Per-forward BatchNorm quantities ([groups][C] each) kept for backward.
-
-    A training-mode finalize may be left *pending* (bn_finalize with the fused path on):
-    the BatchNorm's consumer pass (bn_act) then runs it in its own launch
-    (stf_bn_act_fin).  Reading mean / invstd / scale / shift while it is pending runs
-    the separate finalize first, so every other reader sees the finished values."""
-    __slots__ = ("_mean", "_invstd", "_scale", "_shift", "M", "groups", "training", "_pending")
+    """Per-forward BatchNorm quantities ([groups][C] each) kept for backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "M", "groups", "training")
 
     def __init__(self, C, device, M, groups=1, training=True):
         t = empty((4, groups, C), torch.float32, device)
-        self._mean, self._invstd, self._scale, self._shift = t.unbind(0)
+        self.mean, self.invstd, self.scale, self.shift = t.unbind(0)
         self.M = M
         self.groups = groups
         # training: normalised with the batch statistics (mean / invstd above); eval:
         # with the running statistics, which the backward treats as constants
         self.training = training
-        self._pending = None
-
-    def materialize(self):
-        """Run a pending finalize as its own launch (stf_bn_finalize)."""
-        pend, self._pending = self._pending, None
-        if pend is not None:
-            _FIN_PENDING.pop(id(self), None)
-            d, _stats = pend
-            call("stf_bn_finalize", d.stats, d.tiles, d.groups, d.C, d.M, d.gamma, d.beta, d.momentum, d.eps,
-                 d.running_mean, d.running_var, d.mean, d.invstd, d.scale, d.shift, stream())
-
-    def take_pending(self):
-        """The pending finalize's descriptor, now owned by the caller's fused launch."""
-        pend, self._pending = self._pending, None
-        _FIN_PENDING.pop(id(self), None)
-        return pend[0]
-
-    @property
-    def mean(self):
-        if self._pending is not None:
-            self.materialize()
-        return self._mean
-
-    @property
-    def invstd(self):
-        if self._pending is not None:
-            self.materialize()
-        return self._invstd
-
-    @property
-    def scale(self):
-        if self._pending is not None:
-            self.materialize()
-        return self._scale
-
-    @property
-    def shift(self):
-        if self._pending is not None:
-            self.materialize()
-        return self._shift
 
     @staticmethod
     def identity(C, device):
@@ -608,85 +563,6 @@ class BNState:
         st.scale.fill_(1.0)
         st.shift.zero_()
         return st
-
-
-class _FinDesc(ctypes.Structure):      # stf_bn_fin
-    _fields_ = [("stats", ctypes.c_void_p), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
-                ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
-                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("running_mean", ctypes.c_void_p),
-                ("running_var", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
-                ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p), ("flags", ctypes.c_void_p),
-                ("epoch", ctypes.c_void_p)]
-
-
-class _BwdFinDesc(ctypes.Structure):   # stf_bn_bwd_fin
-    _fields_ = [("partial", ctypes.c_void_p), ("tiles", ctypes.c_int), ("groups", ctypes.c_int), ("C", ctypes.c_int),
-                ("M", ctypes.c_int64), ("gamma", ctypes.c_void_p), ("mean", ctypes.c_void_p),
-                ("invstd", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
-                ("coef", ctypes.c_void_p), ("flags", ctypes.c_void_p), ("epoch", ctypes.c_void_p)]
-
-
-_FIN_PENDING = {}     # id(BNState) -> BNState with a pending finalize (run at flush_batches_tracked)
-_SYNC = {}            # (id(bn module), direction, groups, C, device) -> persistent flags slab (uint32)
-_SLAB_USE = {}        # same key -> host epoch count of its last launch
-_EPOCH = {}           # device index -> [device epoch word (int32, starts at 1), host count of bumps]
-_FIN_OK = {}
-
-
-def fin_fused(M, C, groups):
-    """Whether a training BatchNorm's finalize runs inside its consumer's launch: opt-in
-    (STF_BN_FIN=1), bit-identical to the separate stf_bn_finalize / stf_bn_bwd_finalize
-    launches but measured slower (cfg3 +10 %, cfg2 +4 %: the pass's workgroups wait through the
-    fold), so the separate launches are the default.  A wait that exceeds
-    its spin bound (a broken in-order-dispatch assumption) lets the launch finish with wrong
-    values and sets its slab's sticky word: fin_sync_timeouts() reports it."""
-    if os.environ.get("STF_BN_FIN", "0") != "1":
-        return False
-    key = (M, C, groups)
-    ok = _FIN_OK.get(key)
-    if ok is None:
-        ok = _FIN_OK[key] = bool(_lib.load().stf_bn_fin_ok(M, C, groups))
-    return ok
-
-
-def _epoch(device):
-    key = torch.device(device).index
-    e = _EPOCH.get(key)
-    if e is None:
-        # 1, not 0: a fresh (zeroed) flags slab must not read as published
-        e = _EPOCH[key] = [torch.ones(1, dtype=torch.int32, device=device), 0]
-    return e
-
-
-def fin_epoch_begin(device):
-    """Start a new fused-finalize epoch (the programs call this at the top of every forward and
-    backward, inside what the launch plans record, so each call site's flags slab is used at most
-    once per epoch in replays too)."""
-    if os.environ.get("STF_BN_FIN", "0") == "1":
-        e = _epoch(device)
-        call("stf_bn_fin_epoch_bump", e[0].data_ptr(), stream())
-        e[1] += 1
-
-
-def _fin_slab(bn, direction, C, groups, device):
-    """(flags slab, epoch word) for one fused launch; a second launch of the same call site in one
-    epoch (a caller outside the programs) starts a new epoch first."""
-    key = (id(bn), direction, groups, C, torch.device(device).index)
-    t = _SYNC.get(key)
-    if t is None:
-        t = _SYNC[key] = torch.zeros(_lib.load().stf_bn_fin_flags_words(C, groups), dtype=torch.int32,
-                                     device=device)
-    e = _epoch(device)
-    if _SLAB_USE.get(key) == e[1]:
-        call("stf_bn_fin_epoch_bump", e[0].data_ptr(), stream())
-        e[1] += 1
-    _SLAB_USE[key] = e[1]
-    return t.data_ptr(), e[0].data_ptr()
-
-
-def fin_sync_timeouts():
-    """Number of fused-finalize slabs whose wait ever exceeded its spin bound (sticky last word)."""
-    return int(sum(int(t[-1] != 0) for t in _SYNC.values()))
 
 
 # num_batches_tracked increments are deferred and applied per forward with one
@@ -710,8 +586,6 @@ class _GsumDesc(ctypes.Structure):
 def flush_batches_tracked():
     """End of a training forward: the deferred running-statistics updates of the
     grouped BatchNorms (one stf_bn_running_batch launch) and num_batches_tracked."""
-    for st in list(_FIN_PENDING.values()):      # finalizes no consumer fused (running stats, parked rows)
-        st.materialize()
     if _RUN_PENDING:
         arr = (_RunDesc * len(_RUN_PENDING))(*[d for d, _ in _RUN_PENDING])
         call("stf_bn_running_batch", arr, len(_RUN_PENDING), stream())
@@ -733,11 +607,7 @@ def flush_bn_grads():
 
 def bn_finalize(stats, tiles, bn, M, training, groups=1):
     """``bn`` is the nn.BatchNorm2d holding weight/bias/running stats (its
-    num_batches_tracked advances by ``groups`` at flush_batches_tracked()).
-    Training mode with the fused path (fin_fused): the finalize is left pending on the
-    returned BNState and runs inside the consumer's launch (bn_act), or on the first read
-    of its mean / invstd / scale / shift, or at flush_batches_tracked() -- the running
-    statistics are final once one of those has happened."""
+    num_batches_tracked advances by ``groups`` at flush_batches_tracked())."""
     C = bn.num_features
     st = BNState(C, bn.weight.device, M, groups, training)
     mom = 0.1 if bn.momentum is None else bn.momentum
@@ -749,20 +619,10 @@ def bn_finalize(stats, tiles, bn, M, training, groups=1):
         _RUN_PENDING.append((_RunDesc(stats.data_ptr(), rm.data_ptr(), rv.data_ptr(), M // groups, tiles, groups, C,
                                       float(mom)), (stats, rm, rv)))
         rm = rv = None
-    if training and fin_fused(M, C, groups):
-        # left pending: bn_act runs it inside its own launch (stf_bn_act_fin), any other
-        # reader of the BNState through a separate stf_bn_finalize (BNState.materialize)
-        d = _FinDesc(stats.data_ptr(), tiles, groups, C, M, bn.weight.data_ptr(), bn.bias.data_ptr(), float(mom),
-                     float(bn.eps), _p(rm) if rm is not None else None, _p(rv) if rv is not None else None,
-                     _p(st._mean), _p(st._invstd), _p(st._scale), _p(st._shift),
-                     *_fin_slab(bn, "f", C, groups, bn.weight.device))
-        st._pending = (d, stats)
-        _FIN_PENDING[id(st)] = st
-    else:
-        call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, bn.weight.data_ptr(),
-             bn.bias.data_ptr(), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
-             _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
-             stream())
+    call("stf_bn_finalize", _p(stats) if training else None, tiles, groups, C, M, bn.weight.data_ptr(),
+         bn.bias.data_ptr(), float(mom), float(bn.eps), _p(rm) if rm is not None else None,
+         _p(rv) if rv is not None else None, _p(st.mean), _p(st.invstd), _p(st.scale), _p(st.shift),
+         stream())
     if training and bn.track_running_stats:
         _NBT_PENDING.setdefault(groups, []).append(bn.num_batches_tracked)
     return st
@@ -780,14 +640,6 @@ def bn_act(y: Feat, st: BNState, out: Feat, relu=True, pooled: Feat = None, res:
     if res is not None:
         res.check()
         assert (res.N, res.H, res.W, res.C) == (y.N, y.H, y.W, y.C)
-    if st._pending is not None and (pooled is None or st.groups == 1):
-        rsc = _p(res_st.scale) if res_st is not None else None       # (a pending residual BN runs first)
-        rsh = _p(res_st.shift) if res_st is not None else None
-        d = st.take_pending()
-        call("stf_bn_act_fin", ctypes.byref(d), y.ptr(), y.cs, y.N, y.H, y.W, int(relu),
-             res.ptr() if res is not None else None, res.cs if res is not None else 0, rsc, rsh, out.ptr(), out.cs,
-             pooled.ptr() if pooled is not None else None, stream())
-        return
     call("stf_bn_act", y.ptr(), y.cs, y.N, y.H, y.W, y.C, st.groups, _p(st.scale), _p(st.shift), int(relu),
          res.ptr() if res is not None else None, res.cs if res is not None else 0,
          _p(res_st.scale) if res_st is not None else None, _p(res_st.shift) if res_st is not None else None,
@@ -909,19 +761,6 @@ def bn_backward_from_partial(g: Feat, y: Feat, st: BNState, bn, part, tiles, dga
         _GSUM_PENDING.append((_GsumDesc(part.data_ptr(), dgamma.data_ptr() if dgamma is not None else None,
                                         dbeta.data_ptr() if dbeta is not None else None, tiles, G, C), part))
         dgamma = dbeta = None
-    if st.training and dbias is None and fin_fused(y.M, C, G):
-        # finalize + apply in one launch (stf_bn_bwd_apply_fin)
-        dst = out if out is not None else g
-        if out is not None:
-            out.check()
-            assert (out.N, out.H, out.W, out.C) == (y.N, y.H, y.W, C)
-        if mask_relu:
-            assert out is not None
-        d = _BwdFinDesc(_p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean), _p(st.invstd), _p(dgamma),
-                        _p(dbeta), _p(coef), *_fin_slab(bn, "b", C, G, dev))
-        call("stf_bn_bwd_apply_fin", ctypes.byref(d), g.ptr(), g.cs, y.ptr(), y.cs,
-             _p(st.scale) if mask_relu else None, _p(st.shift) if mask_relu else None, dst.ptr(), dst.cs, stream())
-        return dst
     call("stf_bn_bwd_finalize", _p(part), tiles, G, C, y.M, bn.weight.data_ptr(), _p(st.mean),
          _p(st.invstd), _p(dgamma), _p(dbeta), _p(coef), stream())
     if not st.training:

@@ -341,9 +341,9 @@ class StepRuntime:
         e.dl.copy_(dlogits)
         pos = 0
         hook = p.grad_ready_hook
-        for idx, off in e.marks:
+        for idx, off, deps in e.marks:
             e.bwd.replay(pos, idx)
-            hook(off)
+            hook(off, deps)
             pos = idx
         e.bwd.replay(pos)
 
@@ -360,9 +360,9 @@ class StepRuntime:
         marks = []
         real_hook = p.grad_ready_hook
         if real_hook is not None:
-            def hook(off):
-                marks.append((plan.size(), off))
-                real_hook(off)
+            def hook(off, deps=()):
+                marks.append((plan.size(), off, tuple(deps)))
+                real_hook(off, deps)
             p.grad_ready_hook = hook
 
         def run():

@@ -432,20 +432,22 @@ class STFProgram:
             self._side = side
         return self._side
 
-    def _done(self, module):
+    def _done(self, module, side=None):
+        """The gradients of ``module`` and of everything after it in flat order are final once
+        the current stream's work, the weight-gradient stream's and (``side``) the stream that ran
+        the module's own backward have run: the hook gets those streams as dependencies, so the
+        main stream never waits for a side stream on its account."""
         nhwc.flush_bn_grads()          # grouped BN dgamma/dbeta before the buckets read them
         if self.grad_ready_hook is not None:
-            if self._wstream is not None:       # the bucket reads this module's weight gradients
-                nhwc.wait(torch.cuda.current_stream(), self._wstream)
+            deps = tuple(s for s in (self._wstream, side) if s is not None)
             first = next(module.parameters())
-            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
+            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]], deps)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
         """Refresh the packed weights (one launch) and run the forward schedule."""
         self.packs.refresh()
         nhwc.ACTIVE_PACKS = self.packs
-        nhwc.fin_epoch_begin(x.device)
         try:
             return self._forward(x, training, need_bwd)
         finally:
@@ -453,7 +455,6 @@ class STFProgram:
 
     def backward(self, S, dlogits):
         nhwc.ACTIVE_PACKS = self.packs
-        nhwc.fin_epoch_begin(dlogits.device)
         ws = self._wstream = nhwc.wgrad_side_stream(dlogits.device)
         nhwc.WGRAD_STREAM = ws
         nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device)
@@ -669,14 +670,13 @@ class STFProgram:
             self._done(d)
         dhT[3] = dcur                                          # decoder4 input = h_T of lstm4
         lstm_bwd(3)
-        # join the side streams: all of them now when gradient buckets are being reduced
-        # (ready hooks must arrive in reverse flat order) or PK fusion needs every scale,
-        # else each just before the encoder layer that consumes its d x_t
-        eager = self.grad_ready_hook is not None or P
+        # join the side streams: all of them now when PK fusion needs every scale, else each
+        # just before the encoder layer that consumes its d x_t; a gradient bucket holding lstm k's
+        # gradients waits for side stream k itself (ready-hook dependency), not the main stream
         for k in (3, 2, 1, 0):
-            if eager and k < 3:
+            if P and k < 3:
                 nhwc.wait(main, side[k])
-            self._done(self.lstms[k])
+            self._done(self.lstms[k], side[k] if k < 3 else None)
         if P:
             for k in (3, 2, 1, 0):
                 de[k] = self._pk_fusion_backward(S, k, de[k], gv)
@@ -764,7 +764,7 @@ class _STFFunction(torch.autograd.Function):
             prog.runtime.backward(ctx.saved, dlogits)
         ctx.saved = None
         if prog.grad_ready_hook is not None:
-            prog.grad_ready_hook(0)
+            prog.grad_ready_hook(0, ())
         return (None, None, None, *prog.flat.grad_views())
 
 

@@ -136,17 +136,16 @@ class UNetProgram:
 
     def _done(self, module):
         if self.grad_ready_hook is not None:
-            if nhwc.WGRAD_STREAM is not None:   # the bucket reads this module's weight gradients
-                nhwc.wait(torch.cuda.current_stream(), nhwc.WGRAD_STREAM)
+            # (with weight gradients on a side stream, the bucket waits for that stream too)
+            deps = (nhwc.WGRAD_STREAM,) if nhwc.WGRAD_STREAM is not None else ()
             first = next(module.parameters())
-            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]])
+            self.grad_ready_hook(self.flat.offsets[self.flat.index[id(first)]], deps)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, training, need_bwd):
         """Refresh the packed weights (one launch) and run the forward schedule."""
         self.packs.refresh()
         nhwc.ACTIVE_PACKS = self.packs
-        nhwc.fin_epoch_begin(x.device)
         try:
             return self._forward(x, training, need_bwd)
         finally:
@@ -157,7 +156,6 @@ class UNetProgram:
         # program) measured +1 % at cfg2 but makes every concurrent kernel's duration (and
         # so bench.py's per-kernel roofline) a shared-machine number
         nhwc.ACTIVE_PACKS = self.packs
-        nhwc.fin_epoch_begin(dlogits.device)
         ws = nhwc.wgrad_side_stream(dlogits.device) if os.environ.get("STF_UNET_WGRAD_SIDE") == "1" else None
         nhwc.WGRAD_STREAM = ws
         nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device) if ws is not None else None
@@ -305,7 +303,7 @@ class _UNetFunction(torch.autograd.Function):
             prog.want_dx = False
         ctx.saved = None
         if prog.grad_ready_hook is not None:
-            prog.grad_ready_hook(0)
+            prog.grad_ready_hook(0, ())
         dx, prog.dx = prog.dx, None
         return (dx, None, None, *prog.flat.grad_views())
 

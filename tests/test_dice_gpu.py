@@ -179,3 +179,54 @@ def test_stf_fixed_weight_dice_vs_reference(storage):
         assert d <= 1e-4
     else:
         assert d <= 2 * float(z["fixed_emu_bf16_ddice"]) + 1e-4
+
+
+@pytest.mark.parametrize("storage", [torch.bfloat16, torch.float16])
+def test_stf_frozen_trained_dice_vs_reference(storage):
+    """STF Dice at CONFIDENT trained weights against the reference's own evaluate() (VERDICT r04
+    item 6; tests/golden/stf_trained_frozen.npz, make_golden_trained_stf_frozen.py): the reference
+    trained STFLSTMUNet(T=4) with its ResNet-34 encoder frozen at the canonical init (regenerable from
+    the seed) -- LSTMs, decoders, upconv1, final_res and final trained (6.1 M parameters, committed
+    rounded to bf16, the reference evaluated on exactly those weights) -- then scored 16 held-out
+    [4, 4, 1, 64, 64] batches (65,536 output pixels; median |logit margin| 9.3, 78 pixels < 0.1).
+    bf16 and fp16 storage: |dDice| <= 1e-4, every flipped pixel at a reference margin < 0.1, and the
+    confusion matrix exactly the counts of the run's own argmax."""
+    import os
+    from conftest import GOLDEN
+    from oracle.cases import dce_case
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet, engine
+    z = np.load(os.path.join(GOLDEN, "stf_trained_frozen.npz"))
+    b, t, hw, _, _, n = (int(v) for v in z["config"])
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=t)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    for k, v in sd.items():
+        if "bf16." + k in z.files:
+            bits = z["bf16." + k].astype(np.uint32) << 16
+            sd[k] = torch.from_numpy(bits.view(np.float32).reshape(v.shape).copy())
+        elif "state." + k in z.files:
+            sd[k] = torch.from_numpy(np.asarray(z["state." + k]).copy()).reshape(v.shape).to(v.dtype)
+    assert sum(1 for k in sd if "bf16." + k in z.files) == len(z["trained_keys"])
+    m.load_state_dict(sd)
+    m.storage_dtype = storage
+    m = m.to(DEV)
+    ev = [dce_case(7000 + i, b, t, hw, hw, target_hw=(hw // 2, hw // 2)) for i in range(n)]
+    res = engine.evaluate(m, ev, torch.device(DEV), num_classes=2)
+    preds = []
+    with torch.no_grad():
+        for x5, _ in ev:
+            preds.append(m(engine.preprocess_input(x5, m).to(DEV))["out"].argmax(1).cpu().numpy())
+    shape = tuple(int(v) for v in z["pred_shape"])
+    ref_pred = np.unpackbits(z["pred_bits"])[:int(np.prod(shape))].reshape(shape)
+    flips = np.concatenate(preds) != ref_pred
+    margin = z["margin"].astype(np.float32)
+    worst = float(margin[flips].max()) if flips.any() else 0.0
+    d = abs(res["dice"] - float(z["dice"]))
+    print(f"STF frozen-encoder trained, {storage}: dice {res['dice']:.7f} ref {float(z['dice']):.7f} |d| {d:.2e}, "
+          f"flipped pixels {int(flips.sum())} of {flips.size} (max ref margin {worst:.3g})")
+    tgt = np.concatenate([tt.numpy() for _, tt in ev]).reshape(-1)
+    pred = np.concatenate(preds).reshape(-1)
+    mine = np.bincount(2 * tgt + pred, minlength=4).reshape(2, 2)
+    assert np.array_equal(res["confusion_matrix"].mat.cpu().numpy(), mine)
+    assert worst < 0.1
+    assert d <= 1e-4

@@ -227,3 +227,29 @@ def test_stf_size_fallback_matches_reference():
     with torch.no_grad(), o_q.storage(torch.bfloat16):
         emu = o_emu.forward({k: v.detach() for k, v in p.items()}, x, True)["out"]
     assert emu.shape == out.shape and _rel(emu, g["logits"]) < 0.3
+
+
+def test_stf_frozen_trained_oracle_argmax_vs_reference():
+    """tests/golden/stf_trained_frozen.npz (make_golden_trained_stf_frozen.py: the reference trained
+    STFLSTMUNet(T=4) with its ResNet-34 encoder frozen at the canonical init): the fp32 restatement at
+    the committed weights (canonical encoder + bf16 trained parameters + BatchNorm running statistics)
+    reproduces the reference's per-pixel argmax on all 65,536 held-out pixels -- the fixture the GPU
+    Dice test (tests/test_dice_gpu.py) is held to is consistent with the oracle."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    z = _g("stf_trained_frozen.npz")
+    b, t, hw, _, _, n = (int(v) for v in z["config"])
+    sd = canonical_state_dict(o_stf.template_state_dict(), seed=0)
+    for k, v in sd.items():
+        if "bf16." + k in z.files:
+            sd[k] = torch.from_numpy((z["bf16." + k].astype(np.uint32) << 16).view(np.float32).reshape(v.shape).copy())
+        elif "state." + k in z.files:
+            sd[k] = torch.from_numpy(np.asarray(z["state." + k]).copy()).reshape(v.shape).to(v.dtype)
+    preds = []
+    with torch.no_grad():
+        for i in range(n):
+            x5, _ = dce_case(7000 + i, b, t, hw, hw, target_hw=(hw // 2, hw // 2))
+            preds.append(o_stf.forward(sd, x5, False)["out"].argmax(1).numpy())
+    shape = tuple(int(v) for v in z["pred_shape"])
+    ref = np.unpackbits(z["pred_bits"])[:int(np.prod(shape))].reshape(shape)
+    assert np.array_equal(np.concatenate(preds), ref)
+    assert float(z["dice"]) > 0.95

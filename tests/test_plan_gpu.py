@@ -52,7 +52,10 @@ def _train(which, plan_on, steps=5, pk=False, fp16=False, hook=False, batches=No
         prog = model.program
         snaps = []
         if hook:
-            def h(off):
+            def h(off, deps=()):
+                cur = torch.cuda.current_stream()
+                for st in deps:                 # gradients written on side streams
+                    cur.wait_stream(st)
                 snaps.append((off, prog.flat.grad[off:].clone()))
             prog.grad_ready_hook = h
         losses = []

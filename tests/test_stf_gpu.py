@@ -689,6 +689,65 @@ def test_stf_size_fallback_vs_oracle():
     assert not bad, bad
 
 
+def test_stf_size_fallback_train_vs_reference():
+    """Training mode at 72 x 104 (train-mode BatchNorm at the odd sizes 18x26 / 9x13 / 5x7 / 3x4, the
+    bilinear size fallback in decoder4 / decoder3) on the input of the REFERENCE's own run
+    (tests/golden/stf_t3_72x104.npz, make_golden.py gen_stf_size_fallback):
+      the fp32 restatement, run here on the GPU, reproduces the fixture (logits rel 1e-4, loss 1e-5,
+          every gradient's abs-sum checksum 2e-3: the CPU test's pins, re-checked on this device);
+      the HIP path against it with the full-size train-mode rule (test_stf_fullsize_train_vs_fp32):
+          logits <= 1.3 x the bf16 emulation's error + 0.01, loss within 0.03, every parameter gradient
+          within 2 x the emulation's error + 0.03.  (The reference's own bf16-autocast step is not run
+          here: MIOpen's bf16 batch norm crashes the process at these odd sizes.)"""
+    import oracle.unet_bf16 as o_q
+    from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
+    from oracle.init import canonical_state_dict
+    from stfunet import STFLSTMUNet
+    from stfunet.loss import criterion
+    g = np.load(os.path.join(GOLDEN, "stf_t3_72x104.npz"))
+    m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=3)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).train()
+    sd = {k: v.to(DEV) for k, v in sd.items()}
+    x, t = torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["target"]).to(DEV)
+
+    def params():
+        return {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    p, pe = params(), params()
+    ref = o_stf.forward(p, x, True)["out"]
+    ref_loss = o_loss.criterion(ref, t)
+    ref_loss.backward()
+    # the restatement on this device against the reference's own run
+    assert rel(ref, torch.from_numpy(g["logits"])) < 1e-4
+    assert abs(ref_loss.item() - float(g["loss"])) < 1e-5
+    for k in g.files:
+        if k.startswith("gradck."):
+            ck = float(g[k][1])
+            got = p[k[7:]].grad.double().abs().sum().item()
+            assert abs(got - ck) <= 2e-3 * abs(ck) + 1e-6 * p[k[7:]].numel(), k
+    with o_q.storage(torch.bfloat16):
+        emu = o_emu.forward(pe, x, True)["out"]
+        o_loss.criterion(emu, t).backward()
+    out = m(x)["out"]
+    loss = criterion({"out": out}, t)
+    loss.backward()
+    assert out.shape == ref.shape == (1, 2, 36, 52)
+    e_hip, e_emu = rel(out, ref), rel(emu, ref)
+    bad, errs = [], []
+    for k, prm in m.named_parameters():
+        eh, ee = rel(prm.grad, p[k].grad), rel(pe[k].grad, p[k].grad)
+        errs.append(eh)
+        if eh > 2 * ee + 0.03:
+            bad.append((k, eh, ee))
+    errs.sort()
+    print(f"\nSTF 72x104 train: logits rel {e_hip:.3e} (emu {e_emu:.3e}), loss {loss.item():.6f} vs "
+          f"{ref_loss.item():.6f}; gradient rel median {errs[len(errs) // 2]:.3e}")
+    assert e_hip <= 1.3 * e_emu + 0.01, (e_hip, e_emu)
+    assert abs(loss.item() - ref_loss.item()) < 0.03
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("C,T,B,H", [(64, 5, 3, 6), (128, 8, 16, 32), (256, 8, 16, 16), (512, 8, 16, 8)])
 @pytest.mark.parametrize("gates", [False, True])
 def test_lstm_hoisted_input_projection(monkeypatch, C, T, B, H, gates):
