@@ -933,6 +933,12 @@ __global__ __launch_bounds__(NT) void splitk_reduce_kernel(Geo a, int tpg) {
 // any tap shift (checked exhaustively over columns, shifts and row residues).
 STF_DEV int swzh(int key, int kc) { return kc ^ ((key >> 1) & 2); }
 
+// tap before which the first wave half issues the next stage's DMA share (-1: at the stage start;
+// the second half issues at tap 4); a build-time A/B switch (-DHALO_ATAP=2)
+#ifndef HALO_ATAP
+#define HALO_ATAP -1
+#endif
+
 // output row (pixel index of the destination) of tile pixel p, or -1 outside the image
 template <int PH, int PW, int IX>
 STF_DEV int halo_pixel(int p, int img, int ty, int tx, int Hd, int Wd) {
@@ -1410,7 +1416,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       // LDS-DMA instruction under load, and with all eight waves issuing at once both waves of a
       // SIMD stalled together (DIAG 4: a third of the time); staggered, one wave of each SIMD
       // computes while the other issues
-      if (!STAGGER || !late) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1), wl_next);
+      if (!STAGGER || (!late && HALO_ATAP < 0)) issue(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1), wl_next);
       stamp(2);
     } else {
       // single stage: every wave is done with the buffer, refill it, wait
@@ -1448,7 +1454,7 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
     for (int t = 0; t < 9; ++t) {
       const int b = t & 1;
       if constexpr (STAGGER) {
-        if (t == 4 && late) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
+        if (t == (late ? 4 : HALO_ATAP)) issue(iit, icc, (s + 1) & 1, s + 1 < S && (DIAG != 2 || s < 1), wl_next);
       }
       if (t + 1 < 9) rd_tap(t + 1, b ^ 1);
       // wait for tap t's fragments (the TM + TN tap-t+1 reads may stay in flight)
@@ -1870,11 +1876,11 @@ int halo_ix(const stf_igemm_args* a, bool with_stats);
 int halo_grid(const stf_igemm_args* a, int ix);
 void halo_tiles(const stf_conv_geom& c, int& ty, int& tx);
 
-// deferred epilogue of the second wave half (halo_body DEFER; STF_HALO_DEFER=0: off, A/B).  Its
+// deferred epilogue of the second wave half (halo_body DEFER; default on, STF_HALO_DEFER=0: off, A/B).  Its
 // statistics fold keeps at most 2 (group, slice) keys per workgroup: the item run of a workgroup
 // (items / grid + 1, slice-major, image-major within a slice) must not span more.
 bool halo_defer(const stf_igemm_args* a) {
-  static const int on = [] { const char* e = getenv("STF_HALO_DEFER"); return e ? atoi(e) : 0; }();
+  static const int on = [] { const char* e = getenv("STF_HALO_DEFER"); return e ? atoi(e) : 1; }();
   if (!(on && halo_direct(a) && halo_variant() == 0 && !halo8(a))) return false;
   // (not the two-image 16 x 16 tiles: their deferred variants spill registers)
   const int ix = halo_ix(a, a->stats != nullptr);

@@ -192,16 +192,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
   const int per_img = tiles_y * tiles_x;
 
-  uint4 ra[CHA], rb[CHB], rg[DIAG == 3 ? CHA : 1];
-  // DIAG 3 (timing only, results wrong): the cost side of forming dy = A g mask(y) + B y + C while
-  // staging instead of reading a materialized dy -- a second dy-sized tensor read per tile (another
-  // image's rows: not L2-hot) and the per-element transform with 40 coefficient registers live
-  // (the 5 x 64 coefficients live in LDS: 40 more registers per thread spill the kernel)
-  __shared__ float coefs[DIAG == 3 ? 5 * 64 : 1];
-  if (DIAG == 3) {
-    for (int j = tid; j < 5 * 64; j += NT) coefs[j] = (float)(a.Nout + j) * 1e-4f;
-    __syncthreads();
-  }
+  uint4 ra[CHA], rb[CHB];
   auto load = [&](int t) {
     const int img = t / per_img, rem = t - img * per_img;
     // column-major: the next tile is the one below, whose halo shares two of the (PH + 2)
@@ -217,12 +208,6 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
       ra[i] = make_uint4(0, 0, 0, 0);
       if (yd < a.Hd && xd < a.Wd)
         ra[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
-      if (DIAG == 3) {
-        const int im2 = img + 1 < a.N ? img + 1 : 0;
-        rg[i] = make_uint4(0, 0, 0, 0);
-        if (yd < a.Hd && xd < a.Wd)
-          rg[i] = *reinterpret_cast<const uint4*>(a.dy + (size_t)((im2 * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + ch * 8);
-      }
     }
 #pragma unroll
     for (int i = 0; i < CHB; ++i) {
@@ -239,18 +224,6 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
 #pragma unroll
     for (int i = 0; i < CHA; ++i) {
       const int e = tid + i * NT;
-      if (DIAG == 3) {
-        float yv[8], gv[8];
-        unpack8(ra[i], yv);
-        unpack8(rg[i], gv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float* cf = coefs + (e & 7) * 8 + j;
-          const float gj = yv[j] * cf[192] + cf[256] > 0.f ? gv[j] : 0.f;
-          yv[j] = cf[0] * gj + cf[64] * yv[j] + cf[128];
-        }
-        ra[i] = pack8(yv);
-      }
       *reinterpret_cast<uint4*>(sa + (e >> 3) * SR + (e & 7) * 8) = ra[i];
     }
 #pragma unroll
@@ -346,15 +319,6 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
   }
 
   const int RSC = 9 * a.Cs;
-  if constexpr (DIAG == 4) {
-    if (lane == 0) {
-      const size_t blk = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
-      unsigned long long* d = reinterpret_cast<unsigned long long*>(a.ws) + (blk * 4 + wave) * 4;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) d[k] = tb[k];
-    }
-    return;
-  }
   float* out = a.ws + (size_t)(a.one_slab ? 0 : split) * a.Nout * RSC;
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -369,6 +333,17 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
           out[(size_t)n * RSC + k] = acc[t][i][j][r];
         }
       }
+  if constexpr (DIAG == 4) {
+    // (after the real results, so the MFMA work is not dead code) the buckets overwrite the
+    // first 32 floats of the block's tile: row n0, columns c0.. of tap 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (lane == 0) {
+      unsigned long long* d = reinterpret_cast<unsigned long long*>(out + (size_t)n0 * RSC + c0) + wave * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = tb[k];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -859,8 +834,6 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16 && diag == 2)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);
-    else if (pw == 16 && diag == 3)
-      hipLaunchKernelGGL((wgrad3x3_kernel<16, 3>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16 && diag == 4)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 4>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16)

@@ -68,7 +68,8 @@ class GradAllReduce:
 
     def _ready(self, begin, deps=()):
         """Flat-gradient elements [begin, numel) are final once the current stream's work and
-        that of the streams in ``deps`` (enqueued so far) have run."""
+        that of the streams in ``deps`` (enqueued so far) have run.  Returns whether a bucket was
+        launched (a recording step plan keeps a hook point only where one was)."""
         for s in deps:
             if all(s is not d for d in self.deps):
                 self.deps.append(s)
@@ -78,6 +79,8 @@ class GradAllReduce:
         if self.launched_from - self.ready_from >= self.bucket or self.ready_from == 0:
             self._launch(self.ready_from, self.launched_from)
             self.launched_from = self.ready_from
+            return True
+        return False
 
     def finish(self):
         """Complete every outstanding bucket (call after loss.backward())."""

@@ -359,10 +359,18 @@ class StepRuntime:
         plan = Plan()
         marks = []
         real_hook = p.grad_ready_hook
+        pend = []                       # dependencies of hook calls that launched nothing
         if real_hook is not None:
+            # a hook point splits the replay into segments with a Python call between them; keep
+            # only the points where the hook acted (it returns False when it launched nothing:
+            # its later calls carry those calls' offsets -- the suffix only grows -- and their
+            # dependencies are handed on with the next kept point)
             def hook(off, deps=()):
-                marks.append((plan.size(), off, tuple(deps)))
-                real_hook(off, deps)
+                pend.extend(d for d in deps if all(d is not q for q in pend))
+                acted = real_hook(off, deps)
+                if acted is None or acted:
+                    marks.append((plan.size(), off, tuple(pend)))
+                    pend.clear()
             p.grad_ready_hook = hook
 
         def run():

@@ -671,8 +671,9 @@ class STFProgram:
         dhT[3] = dcur                                          # decoder4 input = h_T of lstm4
         lstm_bwd(3)
         # join the side streams: all of them now when PK fusion needs every scale, else each
-        # just before the encoder layer that consumes its d x_t; a gradient bucket holding lstm k's
-        # gradients waits for side stream k itself (ready-hook dependency), not the main stream
+        # just before the encoder block that first touches its d x_t; a gradient bucket holding
+        # lstm k's gradients waits for side stream k itself (ready-hook dependency), not the main
+        # stream
         for k in (3, 2, 1, 0):
             if P and k < 3:
                 nhwc.wait(main, side[k])
@@ -682,15 +683,18 @@ class STFProgram:
                 de[k] = self._pk_fusion_backward(S, k, de[k], gv)
             self._done(m.pk_fusion1)
         # encoder: layer4 -> layer1; d(layer k-1 output) accumulates into de[k-1]
+        # layer li reads d(its output) = de[li] (lstm li's d x_t, side stream li) and its first
+        # block ACCUMULATES d(its input) into de[li - 1], which lstm li-1's backward writes on side
+        # stream li-1: main waits for each side stream before the first of those two uses
         for li in (3, 2, 1, 0):
             progs, saved = self.layers[li], S.enc[li]
-            if li < 3:
-                nhwc.wait(main, side[li])
-            dout = de[li]
+            dout = de[li]                           # (li < 3: side stream li waited in layer li+1)
             for bi in range(len(progs) - 1, -1, -1):
                 bp, s = progs[bi], saved[bi]
                 if bi == 0:
                     target = de[li - 1] if li > 0 else None
+                    if li > 0 and not P:
+                        nhwc.wait(main, side[li - 1])
                     dout = bp.backward(s, gv, dout=dout, dsrc=target)
                 else:
                     dout = bp.backward(s, gv, dout=dout)

@@ -785,3 +785,38 @@ def test_lstm_hoisted_input_projection(monkeypatch, C, T, B, H, gates):
     for i, (a, b) in enumerate(zip(out["0"][1:], out["1"][1:])):
         e = ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
         assert e <= 2e-3, (i, e)
+
+
+def test_stf_training_steps_repeatable(monkeypatch):
+    """Eight eager training steps, twice from the same weights, with no host sync inside the loop:
+    the losses and the final parameters are identical bit for bit.  The LSTM backwards run on side
+    streams beside the encoder's backward; encoder layer li's first block accumulates into the d x_t
+    of lstm li-1 (side stream li-1), so a missing stream wait shows up here as a nondeterministic
+    loss (a two-rank run of this loop diverged once every ~16 steps, once to NaN, before the wait
+    was placed)."""
+    from stfunet import STFLSTMUNet, engine
+    from stfunet.optim import AdamW
+    from stfunet.synthetic import dce_batch
+    monkeypatch.setenv("STF_PLAN", "0")
+    bs = [dce_batch(2, 4, 128, 128, seed=900 + r, device="cuda", mask_hw=(64, 64)) for r in range(2)]
+
+    def run():
+        torch.manual_seed(0)
+        m = STFLSTMUNet(in_channels=1, num_classes=2, time_steps=4).cuda().train()
+        opt = AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        losses = []
+        for i in range(8):
+            x, t = bs[i % 2]
+            loss = engine.criterion(m(x), t)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.detach().clone())
+        torch.cuda.synchronize()
+        return torch.stack(losses), m.program.flat.data.detach().clone()
+
+    la, pa = run()
+    lb, pb = run()
+    assert torch.isfinite(la).all()
+    assert torch.equal(la, lb), (la, lb)
+    assert torch.equal(pa, pb)
