@@ -869,7 +869,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_pool3_kernel(const uint8_t* __restr
 // the group-major kernels (STF_BN_G=0: the per-unit-division kernels, A/B); usable when C / 8 is
 // a power of two dividing the block and a group's units fit 32-bit indices
 static bool bn_g_ok(long Mg, int C) {
-  static const bool on = [] { const char* e = getenv("STF_BN_G"); return !(e && e[0] == '0'); }();
+  static const bool on = stf::ab_switch("STF_BN_G", 1) != 0;
   const int CG = C / 8;
   return on && C % 8 == 0 && CG > 0 && (CG & (CG - 1)) == 0 && NT % CG == 0 && Mg * CG < (1L << 31);
 }
@@ -987,7 +987,7 @@ extern "C" int stf_bn_bwd_reduce(const void* dz, int dz_cstride, const void* dpo
     STF_CHECK_LAUNCH();
     return 0;
   }
-  static const bool lanes = [] { const char* e = getenv("STF_POOL_LANES"); return !(e && e[0] == '0'); }();
+  static const bool lanes = stf::ab_switch("STF_POOL_LANES", 1) != 0;
   if (dpool && lanes && 64 % (C / 8) == 0 && mask_mode != 2 && (long)N * H * W < (1L << 31))
     hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, grid, dim3(PNT), 0, s, (const uint16_t*)dz, dz_cstride,
                        (const uint16_t*)dpool, (const uint16_t*)y, y_cstride, (long)N, H, W, C, groups, tpg, scale,

@@ -206,6 +206,11 @@ hipError_t memset_async(void* p, int value, size_t bytes, hipStream_t s);
 // STF_WGRAD_ONE_SLAB) take effect only with STF_ABLATION=1 also set; otherwise a set knob is
 // refused with one line on stderr and reads as 0.  Defined in plan.hip.
 int ablation_env(const char* name);
+// A/B switches (results stay valid; each is read once, at its first use).  The complete list, with
+// defaults and what each compares, is DESIGN.md "A/B switches"; nothing else in the library reads
+// the environment.
+int ab_switch(const char* name, int dflt);
+char ab_letter(const char* name);     // first character of the value, 0 when unset
 hipError_t memcpy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
 }  // namespace stf
 

@@ -43,11 +43,6 @@ struct Geo {
   // halo kernel: keep a ring stage's weight rows across items when they are the rows
   // the next fill needs (same 64-channel output slice and source chunk)
   int wkeep;
-  // halo kernel launch knobs: xcd = XCD-aware item ranges (the blocks that share an XCD walk
-  // one contiguous run of items: same output slice -> its weight rows stay in that XCD's L2);
-  // stag = which wave half issues its DMA share at tap 4 (0: odd waves, 1: waves >= NW/2 --
-  // the SIMD partners); prio = s_setprio(1) for waves >= NW/2
-  int xcd, stag, prio;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -1004,18 +999,11 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar DMA addressing
   const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
-  const bool late = (DF || a.stag) ? wave >= NW / 2 : (wave & 1);   // issues its DMA share at tap 4
-  if (a.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const bool late = DF ? wave >= NW / 2 : (wave & 1);   // issues its DMA share at tap 4
   const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
   const int ntiles = (a.N / IX) * tpi;                  // items: channel slice major, pixel tile minor
   const int ipg = a.Mg / (a.Hd * a.Wd);                 // images per statistics group
-  // virtual block id: a bijection of blockIdx.x; every per-block quantity (item range,
-  // statistics row) is keyed by it, so the outputs do not depend on the mapping
-  int vb = blockIdx.x;
-  if (a.xcd && gridDim.x > 8) {
-    const int G = gridDim.x, x = vb & 7, k = vb >> 3, q = G >> 3, r = G & 7;
-    vb = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
-  }
+  const int vb = blockIdx.x;
   const int cnt = per + (int)(vb < rem);
   const int it0 = vb * per + min(vb, rem);
   const int S = cnt * CC;
@@ -1411,8 +1399,8 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
       const bool live = s + 1 < S;
       if (live && ++icc == CC) { icc = 0; ++iit; }
       wl_next = need_w(iit, icc, (s + 1) & 1, live && (DIAG != 2 || s < 1));
-      // the first wave half issues the next stage's DMA now, the second (its SIMD partners;
-      // a.stag = 0: the odd waves) after tap 4: the address path takes ~300 cycles per 1-KiB
+      // the first wave half issues the next stage's DMA now, the second (DF: its SIMD partners,
+      // waves >= NW/2; else the odd waves) after tap 4: the address path takes ~300 cycles per 1-KiB
       // LDS-DMA instruction under load, and with all eight waves issuing at once both waves of a
       // SIMD stalled together (DIAG 4: a third of the time); staggered, one wave of each SIMD
       // computes while the other issues
@@ -1814,35 +1802,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int T
 }
 
 constexpr int HALO_PW = 32;
-// variant: 0 = 16x32 tile, 8 waves, 2-stage ring (1 WG/CU); 1 = 8x32, 4 waves, 1 stage (2 WG/CU)
-int halo_variant() {
-  static const int v = [] { const char* e = getenv("STF_HALO_VARIANT"); return e ? atoi(e) : 0; }();
-  return v;
-}
-int halo_ph() { return halo_variant() == 1 ? 8 : 16; }
+// 16 x 32 tile, 8 waves, 2-stage ring (1 WG/CU)
+constexpr int HALO_PH = 16;
+int halo_ph() { return HALO_PH; }
 // tile width: 32 for W >= 32; 16x16 tiles (32 pixels per wave) for 16 <= W < 32
-int halo_pw(const stf_conv_geom& c) { return (c.Wd >= 32 || halo_variant() == 1) ? HALO_PW : 16; }
-int halo_min_w() {
-  static const int v = [] { const char* e = getenv("STF_HALO_MINW"); return e ? atoi(e) : 16; }();
-  return v;
-}
-// the halo kernel's persistent grid needs enough (pixel tile, 64-channel slice) items to
-// fill the chip; below STF_HALO_MIN_ITEMS the linear kernels (with split-K) run instead
-int halo_min_items() {
-  static const int v = [] { const char* e = getenv("STF_HALO_MIN_ITEMS"); return e ? atoi(e) : 0; }();
-  return v;
-}
-long halo_items(const stf_conv_geom& c, int nout) {
-  const long ty = (c.Hd + halo_ph() - 1) / halo_ph(), tx = (c.Wd + halo_pw(c) - 1) / halo_pw(c);
-  return (long)c.N * ty * tx * (nout / 64);
-}
+int halo_pw(const stf_conv_geom& c) { return c.Wd >= 32 ? HALO_PW : 16; }
+// narrowest layer the halo kernel takes (measured in round 3: at 16 <= W < 32 the 16x16 tile
+// wins up to 256 output channels, the 256x256 linear tile above that)
+constexpr int HALO_MIN_W = 16;
 // 8 x 8 layers through the halo kernel, four images per 8 x 32 tile (conv3x3_halo4_kernel;
 // STF_HALO4=0: the linear split-K kernels, A/B)
 bool halo8(const stf_igemm_args* a) {
-  static const int mode = [] { const char* e = getenv("STF_HALO4"); return e ? atoi(e) : 1; }();
+  static const int mode = stf::ab_switch("STF_HALO4", 1);
   const stf_conv_geom& c = a->g;
   if (mode == 0 || (mode == 2 && a->bnr)) return false;
-  if (halo_variant() != 0 || c.Hd != 8 || c.Wd != 8 || c.N % 4 || a->Nout % 64 || c.Cs % 32) return false;
+  if (c.Hd != 8 || c.Wd != 8 || c.N % 4 || a->Nout % 64 || c.Cs % 32) return false;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
   return (Mg / (c.Hd * c.Wd)) % 4 == 0;
@@ -1850,7 +1824,7 @@ bool halo8(const stf_igemm_args* a) {
 
 // 8-channel-input 3x3 layer through conv3x3_c8_kernel (STF_C8HALO=0: the linear 'e' kernel, A/B)
 bool c8_halo(const stf_igemm_args* a) {
-  static const bool on = [] { const char* e = getenv("STF_C8HALO"); return !(e && e[0] == '0'); }();
+  static const bool on = stf::ab_switch("STF_C8HALO", 1) != 0;
   const stf_conv_geom& c = a->g;
   return on && !a->lstm && !a->scatter2x2 && !c.transposed && !a->bnr && !a->accumulate && c.Cs == 8 &&
          c.src_cstride % 8 == 0 && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs &&
@@ -1861,15 +1835,15 @@ bool c8_halo(const stf_igemm_args* a) {
 // direct-store epilogue; STF_HALO_DIRECT=0 disables, =1 only without BN statistics (dgrad),
 // =2 always (default: measured 1.7 % faster on the forward convs than the LDS-staged one)
 bool halo_direct(const stf_igemm_args* a) {
-  static const int mode = [] { const char* e = getenv("STF_HALO_DIRECT"); return e ? atoi(e) : 2; }();
-  return halo_variant() == 0 && !halo8(a) && (mode == 2 || (mode == 1 && !a->stats));
+  static const int mode = stf::ab_switch("STF_HALO_DIRECT", 2);
+  return !halo8(a) && (mode == 2 || (mode == 1 && !a->stats));
 }
 
 // BN-backward reduction fused into the halo direct epilogue (STF_BNR_FUSED=0: separate
 // stf_bn_bwd_reduce pass after the GEMM, for A/B measurements)
 bool bnr_fused(const stf_igemm_args* a, char k) {
-  static const bool on = [] { const char* e = getenv("STF_BNR_FUSED"); return !(e && e[0] == '0'); }();
-  return on && a->bnr && k == 'H' && halo_direct(a) && halo_variant() == 0;
+  static const bool on = stf::ab_switch("STF_BNR_FUSED", 1) != 0;
+  return on && a->bnr && k == 'H' && halo_direct(a);
 }
 
 int halo_ix(const stf_igemm_args* a, bool with_stats);
@@ -1880,8 +1854,8 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx);
 // statistics fold keeps at most 2 (group, slice) keys per workgroup: the item run of a workgroup
 // (items / grid + 1, slice-major, image-major within a slice) must not span more.
 bool halo_defer(const stf_igemm_args* a) {
-  static const int on = [] { const char* e = getenv("STF_HALO_DEFER"); return e ? atoi(e) : 1; }();
-  if (!(on && halo_direct(a) && halo_variant() == 0 && !halo8(a))) return false;
+  static const int on = stf::ab_switch("STF_HALO_DEFER", 1);
+  if (!(on && halo_direct(a) && !halo8(a))) return false;
   // (not the two-image 16 x 16 tiles: their deferred variants spill registers)
   const int ix = halo_ix(a, a->stats != nullptr);
   if (ix > 1) return false;
@@ -1923,26 +1897,15 @@ constexpr Cfg CFG_F{128, 256, 32};   // 8 waves (2x4), 2 stages, 2 blocks/CU (80
 
 char forced_cfg() {
   static const char c = [] {
-    const char* e = getenv("STF_IGEMM_CFG");
-    return (e && ((e[0] >= 'A' && e[0] <= 'F') || e[0] == 'H' || e[0] == 'L')) ? e[0] : '0';
-  }();
-  return c;
-}
-
-char lstm_forced_cfg() {
-  static const char c = [] {
-    const char* e = getenv("STF_LSTM_CFG");
-    return (e && (e[0] == 'A' || e[0] == 'B' || e[0] == 'C' || e[0] == 'D')) ? e[0] : '\0';
+    const char e = stf::ab_letter("STF_IGEMM_CFG");
+    return ((e >= 'A' && e <= 'F') || e == 'H' || e == 'L') ? e : '0';
   }();
   return c;
 }
 
 // STF_IGEMM_DMA=0 selects the register-staged kernel (A/B comparisons); read once.
 bool dma_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("STF_IGEMM_DMA");
-    return !(e && e[0] == '0');
-  }();
+  static const bool on = stf::ab_switch("STF_IGEMM_DMA", 1) != 0;
   return on;
 }
 
@@ -1957,24 +1920,15 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   const char f = forced_cfg();
   const bool bk64 = c.Cs % 64 == 0;
   if (a->lstm) {
-    // LSTM steps (1x1 GEMM, K = 2C): per-scale tile (STF_LSTM_CFG forces one, A/B);
-    // any tile gives the same gates (same MFMA sequence over ascending K), so the
-    // backward recompute may run a different tile than the forward
-    const char lf = lstm_forced_cfg();
-    char k = lf ? lf : 'A';
-    if (!bk64 && k != 'A') k = 'A';
-    if (k == 'C' && a->lstm->backward) k = 'B';     // the 256x256 tile has no room for the bwd staging
-    return k;
+    // LSTM steps (1x1 GEMM, K = 2C): the 128 x 128 tile (any tile gives the same gates -- the
+    // same MFMA sequence over ascending K -- so the backward recompute may run another tile)
+    return 'A';
   }
   const bool halo_ok = plain && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs &&
                        c.Wd == c.Ws && a->Nout % 64 == 0;
   if (f == 'H' && halo_ok) return 'H';
   // auto: the halo kernel for full-size 3x3 layers ('L' = auto over the linear kernels only)
-  // (measured, tools/ab_minw.sh: at 16 <= W < 32 the 16x16 halo tile wins up to 256 output
-  // channels, the 256x256 linear tile above that)
-  if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= halo_min_w() && a->Nout <= 256)) &&
-      halo_items(c, a->Nout) >= halo_min_items())
-    return 'H';
+  if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= HALO_MIN_W && a->Nout <= 256))) return 'H';
   if (f == '0' && halo_ok && halo8(a)) return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
@@ -2088,11 +2042,11 @@ void halo_tiles(const stf_conv_geom& c, int& ty, int& tx) {
 // with_stats: the launch writes BN statistics (the size queries pass what the launch will do:
 // stf_igemm_stat_tiles is asked before the statistics buffer exists)
 int halo_ix(const stf_igemm_args* a, bool with_stats) {
-  static const int mode = [] { const char* e = getenv("STF_HALO2"); return e ? atoi(e) : 1; }();
+  static const int mode = stf::ab_switch("STF_HALO2", 1);
   const stf_conv_geom& c = a->g;
   if (halo8(a)) return 4;
   if (mode == 0 || (mode == 1 && !with_stats)) return 1;
-  if (halo_variant() != 0 || c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
+  if (c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;
   return ((Mg / (c.Hd * c.Wd)) % 2) ? 1 : 2;
@@ -2104,7 +2058,7 @@ int halo_grid(const stf_igemm_args* a, int ix) {
   halo_tiles(a->g, ty, tx);
   if (ix > 1) ty = tx = 1;
   const long items = (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
-  return (int)std::min<long>(items, (long)num_cus() * (halo_variant() == 1 || ix == 4 ? 2 : 1));
+  return (int)std::min<long>(items, (long)num_cus() * (ix == 4 ? 2 : 1));
 }
 
 // Split-K factor for a plain gather on the linear DMA kernels that would leave the
@@ -2112,7 +2066,7 @@ int halo_grid(const stf_igemm_args* a, int ix) {
 // K slices until ~256 workgroups, each keeping >= 8 K steps.  1 = no split.
 // STF_SPLITK=0 disables it (A/B).
 int ksplit_of(const stf_igemm_args* a) {
-  static const bool on = [] { const char* e = getenv("STF_SPLITK"); return !(e && e[0] == '0'); }();
+  static const bool on = stf::ab_switch("STF_SPLITK", 1) != 0;
   const stf_conv_geom& c = a->g;
   const char k = choose(a, dma_fits(a));
   if (!on || a->lstm || a->scatter2x2 || c.transposed || c.Cs == 8) return 1;
@@ -2177,8 +2131,6 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
       else if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false", halo_defer(a) ? "true" : "false");
-      else if (halo_variant() == 1)
-        snprintf(buf, sizeof buf, "conv3x3_halo_kernel<8, %d, 4, 1, 0, 0, false, false>", HALO_PW);
       else
         snprintf(buf, sizeof buf, "conv3x3_halo_kernel<16, %d, 8, 2, 0, %d, %s, %s>", halo_pw(c),
                  halo_direct(a) ? (a->stats ? 2 : 1) : 0, bnr_fused(a, k) ? "true" : "false",
@@ -2242,12 +2194,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.bnr_relu = 0; g.bnr_part = nullptr;
   g.par = 0;
   g.ksplit = 1; g.ws = nullptr;
-  static const int wkeep = [] { const char* e = getenv("STF_HALO_WKEEP"); return e ? atoi(e) : 1; }();
+  static const int wkeep = stf::ab_switch("STF_HALO_WKEEP", 1);
   g.wkeep = wkeep;
-  static const int xcd = [] { const char* e = getenv("STF_HALO_XCD"); return e ? atoi(e) : 0; }();
-  static const int stag = [] { const char* e = getenv("STF_HALO_STAG"); return e ? atoi(e) : 0; }();
-  static const int prio = [] { const char* e = getenv("STF_HALO_PRIO"); return e ? atoi(e) : 0; }();
-  g.xcd = xcd; g.stag = stag; g.prio = prio;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
@@ -2291,14 +2239,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     const long items = (long)(c.N / ix) * ty * tx * (a->Nout / 64);
     const int grid = halo_grid(a, ix);
     static const int diag = stf::ablation_env("STF_HALO_DIAG");
-#define STF_H(D) do {                                                                                            \
-    if (halo_variant() == 1)                                                                                     \
-      hipLaunchKernelGGL((conv3x3_halo_kernel<8, HALO_PW, 4, 1, D>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, \
-                         tx, (int)(items / grid), (int)(items % grid));                                          \
-    else                                                                                                         \
-      hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, src_bytes,   \
-                         ty, tx, (int)(items / grid), (int)(items % grid));                                      \
-  } while (0)
+#define STF_H(D) hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, \
+                                   src_bytes, ty, tx, (int)(items / grid), (int)(items % grid))
     const int d = halo_direct(a) ? (a->stats ? 2 : 1) : 0;
     const int per = (int)(items / grid), rem = (int)(items % grid);
     const bool dfr = halo_defer(a);
@@ -2348,11 +2290,11 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   }
   // stride-2 transposed gathers: rows by output parity class, only that class's taps
   // (STF_TRANS_PAR=0: all nine taps, 3/4 of them masked)
-  static const bool par_on = [] { const char* e = getenv("STF_TRANS_PAR"); return !(e && e[0] == '0'); }();
+  static const bool par_on = stf::ab_switch("STF_TRANS_PAR", 1) != 0;
   if (par_on && c.transposed && c.stride == 2 && (k == 'A' || k == 'E') && g.Mg == g.M) {
     const int bmp = cfg_of(k).bm;
     // accumulating: tap-less classes add nothing, skip them (STF_TRANS_SKIP=0: launch them, A/B)
-    static const bool skip_on = [] { const char* e = getenv("STF_TRANS_SKIP"); return !(e && e[0] == '0'); }();
+    static const bool skip_on = stf::ab_switch("STF_TRANS_SKIP", 1) != 0;
     // (only when the epilogue adds nothing of its own: no bias, statistics or fused BN reduce)
     const int par = a->accumulate && skip_on && !a->bias && !a->stats && !a->bnr ? 2 : 1;
     long blocks = 0;

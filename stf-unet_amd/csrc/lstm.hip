@@ -386,13 +386,8 @@ extern "C" int stf_lstm_seq_fwd(const void* wcat, const float* bias, void* lbuf,
   if (C != 64 || !wcat || !bias || !lbuf || !c_out || !h_last || h_cstride < C) return STF_EINVAL;
   if (((uintptr_t)wcat & 15) || ((uintptr_t)lbuf & 15) || ((uintptr_t)c_out & 15)) return STF_EINVAL;
   const dim3 grid((P + BM - 1) / BM);
-  static const int occ = [] { const char* e = getenv("STF_LSTM_OCC"); return e ? atoi(e) : 2; }();
-  if (occ == 1)
-    hipLaunchKernelGGL((lstm_seq_fwd_kernel<64, 1>), grid, dim3(NT), 0, (hipStream_t)stream, (const uint16_t*)wcat,
-                       bias, (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride);
-  else
-    hipLaunchKernelGGL((lstm_seq_fwd_kernel<64, 2>), grid, dim3(NT), 0, (hipStream_t)stream, (const uint16_t*)wcat,
-                       bias, (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride);
+  hipLaunchKernelGGL((lstm_seq_fwd_kernel<64, 2>), grid, dim3(NT), 0, (hipStream_t)stream, (const uint16_t*)wcat,
+                     bias, (uint16_t*)lbuf, P, T, c_out, (uint16_t*)h_last, h_cstride);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -156,6 +156,16 @@ int stf::ablation_env(const char* name) {
   return 0;
 }
 
+int stf::ab_switch(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && e[0]) ? atoi(e) : dflt;
+}
+
+char stf::ab_letter(const char* name) {
+  const char* e = getenv(name);
+  return e ? e[0] : 0;
+}
+
 hipError_t stf::memset_async(void* p, int value, size_t bytes, hipStream_t s) {
   if (!g_rec) return hipMemsetAsync(p, value, bytes, s);
   auto* op = new MemsetOp;

@@ -707,7 +707,7 @@ bool big_tile(const stf_wgrad_args* a) { return a->Nout % 128 == 0 && a->g.Cs % 
 
 // fused-tap kernel: 3x3, stride 1, pad 1, 64-multiples of channels, W >= 8
 int fused_pw(const stf_wgrad_args* a) {
-  static const bool enabled = [] { const char* e = getenv("STF_WGRAD_FUSED"); return !(e && e[0] == '0'); }();
+  static const bool enabled = stf::ab_switch("STF_WGRAD_FUSED", 1) != 0;
   const stf_conv_geom& c = a->g;
   if (!enabled) return 0;
   if (c.R != 3 || c.S != 3 || c.stride != 1 || c.pad != 1 || c.Hd != c.Hs || c.Wd != c.Ws) return 0;
@@ -718,7 +718,7 @@ int fused_pw(const stf_wgrad_args* a) {
 // LDS-DMA staging for the fused 3x3 kernel (STF_WGRAD_DMA=0: register staging, A/B);
 // buffer offsets are 32-bit
 bool wgrad_dma(const stf_wgrad_args* a) {
-  static const bool on = [] { const char* e = getenv("STF_WGRAD_DMA"); return e && e[0] == '1'; }();
+  static const bool on = stf::ab_switch("STF_WGRAD_DMA", 0) == 1;
   const stf_conv_geom& c = a->g;
   return on && (uint64_t)c.N * c.Hd * c.Wd * a->dy_cstride * 2 < 0xFFFFFF00ull &&
          (uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2 < 0xFFFFFF00ull;
@@ -726,7 +726,7 @@ bool wgrad_dma(const stf_wgrad_args* a) {
 
 // ConvT 2x2 / stride 2 fused-tap kernel (x = the 2x larger gradient tensor)
 int fused22_pw(const stf_wgrad_args* a) {
-  static const bool enabled = [] { const char* e = getenv("STF_WGRAD_FUSED"); return !(e && e[0] == '0'); }();
+  static const bool enabled = stf::ab_switch("STF_WGRAD_FUSED", 1) != 0;
   const stf_conv_geom& c = a->g;
   if (!enabled || c.R != 2 || c.S != 2 || c.stride != 2 || c.pad != 0 || c.transposed) return 0;
   if (c.Hs != 2 * c.Hd || c.Ws != 2 * c.Wd || a->Nout % 64 || c.Cs % 64 || c.Wd < 8) return 0;
@@ -738,8 +738,7 @@ int fused22_pw(const stf_wgrad_args* a) {
 // of a pixel tile meet in L2 anyway and the 3-per-CU occupancy wins, 150 vs 172 us).
 // STF_WGRAD22_NB=1: always 1 (A/B)
 int fused22_nb(const stf_wgrad_args* a) {
-  static const int force1 = [] { const char* e = getenv("STF_WGRAD22_NB"); return e && e[0] == '1'; }();
-  return (!force1 && a->Nout % 128 == 0 && a->Nout >= 256) ? 2 : 1;
+  return (a->Nout % 128 == 0 && a->Nout >= 256) ? 2 : 1;
 }
 
 void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
@@ -812,8 +811,7 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.N = c.N; w.Hs = c.Hs; w.Ws = c.Ws; w.Cs = c.Cs; w.xcs = c.src_cstride; w.Hd = c.Hd; w.Wd = c.Wd;
   w.R = c.R; w.S = c.S; w.st = c.stride; w.pad = c.pad; w.M = c.N * c.Hd * c.Wd; w.Nout = a->Nout;
   w.dycs = a->dy_cstride; w.chunk = chunk;
-  static const int colmajor = [] { const char* e = getenv("STF_WGRAD_COLMAJOR"); return e ? atoi(e) : 1; }();
-  w.colmajor = colmajor;
+  w.colmajor = 1;
   // timing-only ablation: the split-K slabs of the fused 3x3 kernel all land in slab 0 (L2-resident:
   // no slab traffic to HBM; the sums are wrong) -- the upper bound of folding the slabs in-kernel
   static const int one_slab = stf::ablation_env("STF_WGRAD_ONE_SLAB") == 1;
@@ -874,10 +872,8 @@ extern "C" int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, i
   if (total % 8 || ((uintptr_t)ws & 15)) return STF_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int rs = R * S;
-  static const int mode = [] { const char* e = getenv("STF_WRED_MODE"); return e ? atoi(e) : -1; }();
   const bool shape_ok = (rs == 9 || rs == 4 || rs == 1) && ((long)Nout * Cs) % 4 == 0;
-  const int m = mode >= 0 ? mode : (shape_ok && splits <= 8) ? 2 : 0;
-  if (m == 2 && shape_ok) {
+  if (shape_ok && splits <= 8) {
     const unsigned blocks = (unsigned)(((long)Nout * Cs / 4 * rs + 255) / 256);
     if (rs == 9) hipLaunchKernelGGL(wgrad_reduce_tap_kernel<9>, dim3(blocks), dim3(256), 0, s, ws, splits, Nout, Cs, out);
     else if (rs == 4) hipLaunchKernelGGL(wgrad_reduce_tap_kernel<4>, dim3(blocks), dim3(256), 0, s, ws, splits, Nout, Cs, out);
