@@ -6,16 +6,19 @@ process per GPU runs the same program on its own batch; BatchNorm statistics
 stay per rank (torch DDP's default, no SyncBN in the reference).  Gradients live
 in one flat fp32 buffer and backward finishes parameter blocks in reverse flat
 order, so the finished gradients always form a suffix of that buffer: as soon as
-``bucket_mb`` of new suffix is final, an async all-reduce of that contiguous
-slice is enqueued (RCCL runs it on its own stream after an event wait on the
-compute stream) while the remaining backward kernels keep the GPU busy.
-``finish()`` reduces the last bucket and makes the compute stream wait.
+``bucket_mb`` of new suffix is final, an all-reduce of that contiguous slice is
+enqueued while the remaining backward kernels keep the GPU busy.  ``finish()``
+reduces the last bucket and makes the compute stream wait.
 
 Gradients written on side streams (the STF program's LSTM backwards and weight-gradient
-stream) reach the hook as ``deps``: the bucket that contains them is launched from a joiner
-stream that waits for the compute stream AND those streams, so the compute stream itself
-never waits for a side stream on the hook's account (the schedule with the hook attached is
-the schedule without it).
+stream) reach the hook as ``deps``.  A bucket's collective is enqueued ON the joiner stream
+(``async_op=False`` under it: RCCL launches on the current stream, the host does not block),
+after the joiner waits for the compute stream and those side streams -- so the compute stream
+never waits for a side stream on the hook's account, and no stream of RCCL's own is involved:
+on HIP, streams share GPU_MAX_HW_QUEUES hardware queues (4) and two streams on one queue run in
+order, so a collective stream that lands on the compute stream's queue turns its event wait into
+a join of the side streams (the STF step was 3-5 % slower with the hook that way; the joiner
+and the programs' side streams are high-priority streams, a queue pool of their own).
 
 Buckets are large and few on purpose: xGMI is point-to-point (7 links per GPU),
 RCCL's ring/tree bandwidth per call grows with message size, and each call costs
@@ -33,7 +36,11 @@ class GradAllReduce:
         self.group = group
         self.world = dist.get_world_size(group)
         self.bucket = max(1, int(bucket_mb * (1 << 20) // 4))
-        self.avg = dist.get_backend(group) == "nccl"
+        # RCCL's AVG is one fused pass (pre-multiplied sum); gloo has no AVG (SUM, then a divide).
+        # One rank: SUM in place is no work at all, while RCCL's one-rank AVG still launches a
+        # scaling kernel over every bucket (oneRankReduce, ~107 us per 54 MB bucket on MI355X)
+        # that contends with the backward for CUs and changes nothing
+        self.avg = dist.get_backend(group) == "nccl" and self.world > 1
         self.prog.grad_ready_hook = self._ready
         self._reset()
 
@@ -44,10 +51,8 @@ class GradAllReduce:
         self.deps = []                  # side streams the next bucket must wait for
 
     def _joiner(self, dev):
-        j = getattr(self, "_join", None)
-        if j is None or j.device != dev:
-            j = self._join = torch.cuda.Stream(device=dev)
-        return j
+        from .nhwc import side_stream
+        return side_stream(dev, "ddp_join")
 
     def _launch(self, lo, hi):
         if hi <= lo:
@@ -55,16 +60,16 @@ class GradAllReduce:
         t = self.flat.grad[lo:hi]
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
         deps, self.deps = self.deps, []
-        if deps and t.is_cuda:
+        if t.is_cuda:
             js = self._joiner(t.device)
             js.wait_stream(torch.cuda.current_stream(t.device))
             for s in deps:
                 js.wait_stream(s)
             with torch.cuda.stream(js):
-                w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+                dist.all_reduce(t, op=op, group=self.group, async_op=False)
+            self.works.append((None, t))
         else:
-            w = dist.all_reduce(t, op=op, group=self.group, async_op=True)
-        self.works.append((w, t))
+            self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t))
 
     def _ready(self, begin, deps=()):
         """Flat-gradient elements [begin, numel) are final once the current stream's work and
@@ -86,8 +91,14 @@ class GradAllReduce:
         """Complete every outstanding bucket (call after loss.backward())."""
         if self.launched_from is not None and self.launched_from > 0:
             self._launch(0, self.launched_from)
+        joined = set()
         for w, t in self.works:
-            w.wait()
-            if not self.avg:
+            if w is None:
+                if t.device not in joined:
+                    torch.cuda.current_stream(t.device).wait_stream(self._joiner(t.device))
+                    joined.add(t.device)
+            else:
+                w.wait()
+            if not self.avg and self.world > 1:
                 t.div_(self.world)
         self._reset()

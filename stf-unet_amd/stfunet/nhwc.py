@@ -440,7 +440,27 @@ def rows(f: Feat, n0, n):
 
 
 WGRAD_STREAM = None   # set by a program: weight gradients run there, off the critical path
-_WSTREAMS = {}
+_STREAMS = {}
+
+
+def side_stream(device, name):
+    """The process's side stream ``name`` on ``device``: the programs' side streams, the
+    weight-gradient stream and the DDP joiner, one each per process however many programs are
+    built.  High priority: HIP puts high-priority streams in a hardware-queue pool of their own,
+    so a side stream never shares (and is never serialized behind) the caller's compute stream's
+    queue, whatever streams the process made before -- e.g. RCCL's, which shifted the STF side
+    streams onto the compute stream's queue (STF_SIDE_PRIO=0: normal priority, A/B)."""
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index, name)
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.Stream(device=dev, priority=_SIDE_PRIO)
+    return st
+
+
+_SIDE_PRIO = int(os.environ.get("STF_SIDE_PRIO", "-1"))
 
 
 def wgrad_side_stream(device):
@@ -449,10 +469,7 @@ def wgrad_side_stream(device):
     inline, for A/B measurements)."""
     if os.environ.get("STF_WGRAD_SIDE", "1") == "0":
         return None
-    key = torch.device(device).index
-    if key not in _WSTREAMS:
-        _WSTREAMS[key] = torch.cuda.Stream(device=device)
-    return _WSTREAMS[key]
+    return side_stream(device, "wgrad")
 
 
 def wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, defer=True):

@@ -427,7 +427,7 @@ class STFProgram:
                     side.append(ws)
                 else:
                     if c not in own:
-                        own[c] = torch.cuda.Stream(device=dev)
+                        own[c] = nhwc.side_stream(dev, "side" + c)
                     side.append(own[c])
             self._side = side
         return self._side
