@@ -1634,12 +1634,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo2_kernel(Geo a, uint32_t s
   halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2, DEFER>(a, src_bytes, TY, TX, per, rem);
 }
 
-// four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves, one stage, two workgroups
-// per CU (61 KB of LDS each)
-template <int DIRECT>
-__global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
-                                                               int rem) {
-  halo_body<8, 32, 4, 1, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
+// four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves.  ST = 1: one stage, two
+// workgroups per CU (61 KB of LDS each) -- one workgroup's DMA waits hide behind the other's
+// MFMAs; ST = 2: a 2-stage ring, one workgroup per CU (123 KB), for grids that would not put two
+// workgroups on every CU (STF cfg3: 256 items)
+template <int DIRECT, int ST>
+__global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_halo4_kernel(Geo a, uint32_t src_bytes, int TY,
+                                                                             int TX, int per, int rem) {
+  halo_body<8, 32, 4, ST, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
 }
 
 // ---------------------------------------------------------------------------
@@ -2052,13 +2054,25 @@ int halo_ix(const stf_igemm_args* a, bool with_stats) {
   return ((Mg / (c.Hd * c.Wd)) % 2) ? 1 : 2;
 }
 
-// persistent halo grid: one workgroup per CU (160 KiB LDS each)
-int halo_grid(const stf_igemm_args* a, int ix) {
+long halo_items_ix(const stf_igemm_args* a, int ix) {
   int ty, tx;
   halo_tiles(a->g, ty, tx);
   if (ix > 1) ty = tx = 1;
-  const long items = (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
-  return (int)std::min<long>(items, (long)num_cus() * (ix == 4 ? 2 : 1));
+  return (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
+}
+
+// stages of the 8 x 8 (IX = 4) halo kernel: the single-stage kernel relies on two workgroups per
+// CU, so with fewer items than 2 x CUs the 2-stage ring runs instead (STF_HALO4_ST=1 / 2 forces one)
+int halo4_stages(const stf_igemm_args* a) {
+  static const int force = stf::ab_switch("STF_HALO4_ST", 0);
+  if (force == 1 || force == 2) return force;
+  return halo_items_ix(a, 4) < 2L * num_cus() ? 2 : 1;
+}
+
+// persistent halo grid: one workgroup per CU (160 KiB LDS each; the single-stage 8 x 8 kernel two)
+int halo_grid(const stf_igemm_args* a, int ix) {
+  const long items = halo_items_ix(a, ix);
+  return (int)std::min<long>(items, (long)num_cus() * (ix == 4 && halo4_stages(a) == 1 ? 2 : 1));
 }
 
 // Split-K factor for a plain gather on the linear DMA kernels that would leave the
@@ -2127,7 +2141,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
     case 'K': snprintf(buf, sizeof buf, "conv3x3_c8_kernel"); break;
     case 'H':
       if (halo8(a))
-        snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
+        snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0, %d>", halo4_stages(a));
       else if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false", halo_defer(a) ? "true" : "false");
@@ -2257,7 +2271,10 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
                               rem);                                                                                    \
     } while (0)
     if (ix == 4) {
-      hipLaunchKernelGGL((conv3x3_halo4_kernel<0>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
+      if (halo4_stages(a) == 2)
+        hipLaunchKernelGGL((conv3x3_halo4_kernel<0, 2>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
+      else
+        hipLaunchKernelGGL((conv3x3_halo4_kernel<0, 1>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
     } else if (ix > 1) {
       if (bnr_fused(a, k)) STF_H2(1, true);
       else if (d == 2) STF_H2(2, false);
