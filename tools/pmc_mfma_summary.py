@@ -10,6 +10,11 @@ Per dispatch (counters summed over the chip by rocprofv3):
   * util_flop  = mfma_flop / (cycles x 1024 SIMDs x 1024 FLOP/clk/SIMD): the dense-bf16 fraction at
                  the clock actually held (2.5 PF at 2.4 GHz = 1024 FLOP/clk per SIMD)
   * frac_2p5   = mfma_flop / duration / 2.5 PF: the same work against the datasheet peak
+A dispatch's own quotient reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS
+give-back), so the step clock -- sum of cycles / sum of durations over the run's dispatches of at least
+0.3 ms -- is also reported, and every kernel's MFMA busy fraction is given at that clock too
+(``mfma_busy_util_step_clock`` = busy cycles / (step clock x duration x 1024 SIMDs)): for the short
+STF dispatches that is the number to read.
 Profiled passes clock ~2-5 % below un-profiled runs (MI355X_MICROARCH.md, DVFS item 2), so the
 absolute TF/s here read low; the utilisation ratios are per cycle and do not depend on it.
 """
@@ -75,13 +80,34 @@ def main():
         g["dur_ns"] += e["dur_ns"]
         for c in COUNTERS:
             g[c] += e[c]
+    long_ = [e for e in ev if e["dur_ns"] >= 3e5]
+    # cycles_i = clock x duration_i + c0 over every dispatch of the run (least squares): the slope
+    # is the clock, the intercept the per-dispatch over-read that inflates short dispatches' quotient
+    xs = [e["dur_ns"] for e in ev]
+    ys = [e["GRBM_GUI_ACTIVE"] / 8.0 for e in ev]
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    sxx = sum((x - mx) ** 2 for x in xs)
+    fit_clock = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx if sxx else 0.0
+    fit_c0 = my - fit_clock * mx
+    if len(long_) >= 10:
+        step_clock = sum(e["GRBM_GUI_ACTIVE"] / 8.0 for e in long_) / sum(e["dur_ns"] for e in long_)
+        clock_from = f"{len(long_)} dispatches of >= 0.3 ms (sum of GRBM_GUI_ACTIVE/8 / sum of durations)"
+    else:
+        step_clock = fit_clock
+        clock_from = (f"slope of GRBM_GUI_ACTIVE/8 against duration over all {n} dispatches (fewer than 10 "
+                      f"of >= 0.3 ms; intercept {fit_c0:.0f} cycles per dispatch)")
     kernels = {}
     for k, g in sorted(agg.items(), key=lambda kv: -kv[1]["dur_ns"]):
         d = derive(g)
         if d["mfma_flop"] <= 0:
             continue
-        kernels[k] = {"launches": int(g["launches"]), "avg_us": round(g["dur_ns"] / g["launches"] / 1e3, 2),
-                      "clock_ghz": round(d["clock_ghz"], 3), "mfma_busy_util": round(d["mfma_util"], 4),
+        avg_ns = g["dur_ns"] / g["launches"]
+        kernels[k] = {"launches": int(g["launches"]), "avg_us": round(avg_ns / 1e3, 2),
+                      "clock_ghz": round(d["clock_ghz"], 3), "clock_reliable": avg_ns >= 3e5,
+                      "mfma_busy_util_step_clock": round(g["SQ_VALU_MFMA_BUSY_CYCLES"] /
+                                                        (step_clock * g["dur_ns"] * SIMDS), 4) if step_clock else None,
+                      "mfma_busy_util": round(d["mfma_util"], 4),
                       "mfma_flop_util_at_clock": round(d["util_flop"], 4), "tflops": round(d["tflops"], 1),
                       "frac_of_2p5PF": round(d["tflops"] / 2500.0, 4)}
     res = {"workload": a.workload, "command": a.command,
@@ -89,9 +115,12 @@ def main():
                      "--kernel-trace (one pass); cycles = GRBM_GUI_ACTIVE/8; mfma_busy_util = MFMA busy "
                      "cycles / (cycles x 1024 SIMDs); mfma_flop_util_at_clock = MOPS_BF16*512 / (cycles x "
                      "1024 SIMDs x 1017 FLOP/clk); frac_of_2p5PF = MFMA FLOP / duration / 2.5 PF",
+           "step_clock_ghz": round(step_clock, 3),
+           "step_clock_from": clock_from,
+           "fit_clock_ghz": round(fit_clock, 3), "fit_overread_cycles_per_dispatch": round(fit_c0),
            "kernels": kernels}
     if a.unet_layers:
-        halo = [e for e in ev if e["name"] == "conv3x3_halo_kernel<16, 32, 8, 2, 0, 2, false>"]
+        halo = [e for e in ev if e["name"].startswith("conv3x3_halo_kernel<16, 32, 8, 2, 0, 2, false")]
         n = len(UNET_FWD_HALO)
         layers = defaultdict(list)
         for i, e in enumerate(halo[(len(halo) // n - 1) * n:]):   # the last profiled step
@@ -104,10 +133,16 @@ def main():
     os.makedirs(os.path.dirname(os.path.abspath(a.json)), exist_ok=True)
     with open(a.json, "w") as f:
         json.dump(res, f, indent=1)
-    print(f"{'kernel':60s} {'n':>4s} {'avg us':>8s} {'GHz':>6s} {'busy':>6s} {'flop@clk':>8s} {'TF/s':>7s} {'/2.5PF':>6s}")
+    print(f"step clock {step_clock:.3f} GHz from {clock_from}; fit over all dispatches: "
+          f"{fit_clock:.3f} GHz + {fit_c0:.0f} cycles per dispatch")
+    print(f"{'kernel':60s} {'n':>4s} {'avg us':>8s} {'GHz':>6s} {'busy':>6s} {'busy@step':>9s} {'flop@clk':>8s} "
+          f"{'TF/s':>7s} {'/2.5PF':>6s}")
     for k, v in list(kernels.items())[:20]:
-        print(f"{k[:60]:60s} {v['launches']:4d} {v['avg_us']:8.1f} {v['clock_ghz']:6.3f} {v['mfma_busy_util']:6.3f} "
+        bs = v["mfma_busy_util_step_clock"]
+        print(f"{k[:60]:60s} {v['launches']:4d} {v['avg_us']:8.1f} {v['clock_ghz']:6.3f}{'' if v['clock_reliable'] else '*'}"
+              f"{v['mfma_busy_util']:6.3f} {bs if bs is not None else float('nan'):9.3f} "
               f"{v['mfma_flop_util_at_clock']:8.3f} {v['tflops']:7.1f} {v['frac_of_2p5PF']:6.3f}")
+    print("(* = average dispatch under 0.3 ms: its own clock reads high; use busy@step)")
     for k, v in res.get("forward_halo_layers_last_step", {}).items():
         print(f"  {k:8s} {v['us']:7.1f} us  {v['clock_ghz']:.3f} GHz  busy {v['mfma_busy_util']:.3f}  "
               f"flop@clk {v['mfma_flop_util_at_clock']:.3f}  {v['tflops']:.0f} TF/s")
