@@ -9,7 +9,12 @@ buffer and the data-parallel all-reduce moves contiguous buckets.
 Slices are 16-byte aligned (offsets rounded up to 4 floats) for float4 access;
 the gaps stay zero in both buffers.
 """
+import operator
+
 import torch
+
+
+_REQ = operator.attrgetter("requires_grad")
 
 
 def _align4(n):
@@ -82,6 +87,9 @@ class FlatParams:
             self._spare = self.grad
             self._use(other)
         self.grad.zero_()
+
+    def any_requires_grad(self):
+        return any(map(_REQ, self.params))
 
     def grad_view(self, p):
         return self._views[self.index[id(p)]]

@@ -317,6 +317,15 @@ class StepRuntime:
         self.cur = e
         return e.logits, e.S
 
+    def own(self, S, ctx):
+        """``ctx`` (an autograd ctx) now holds the state ``S`` that forward just returned: when that
+        is a plan entry's static state, the entry is busy until ctx's backward (forward's ``ctx``
+        argument, given after the launches -- the models enqueue the replay before autograd's
+        per-parameter bookkeeping)."""
+        e = self.cur
+        if e is not None and S is not None and e.S is S:
+            e.owner = weakref.ref(ctx)
+
     def _record_forward(self, e, x, training):
         with _no_gc():
             self._record_forward_pooled(e, x, training)

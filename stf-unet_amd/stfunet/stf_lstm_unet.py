@@ -747,14 +747,13 @@ def _check_input_shape(shape, P):
 
 
 class _STFFunction(torch.autograd.Function):
+    """``res`` = (logits, saved state) of the forward STFLSTMUNet.forward already enqueued: the GPU
+    starts on the step while autograd processes the ~160 parameter inputs of this call (~100 us of
+    host time at every synced step boundary)."""
     @staticmethod
-    def forward(ctx, x, prog, storage, *params):
-        if ctx.needs_input_grad[0]:
-            raise NotImplementedError("stfunet.STFLSTMUNet computes parameter gradients only; the input "
-                                      "sequence must not require grad")
-        need_bwd = any(ctx.needs_input_grad[3:])
-        with _lib.storage(storage):
-            logits, saved = prog.runtime.forward(x, prog.m.training, need_bwd, ctx)
+    def forward(ctx, x, prog, storage, res, *params):
+        logits, saved = res
+        prog.runtime.own(saved, ctx)
         ctx.storage = storage
         ctx.prog, ctx.saved = prog, saved
         return logits.detach()        # the plan's static logits: a fresh tensor object per step
@@ -769,7 +768,7 @@ class _STFFunction(torch.autograd.Function):
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0, ())
-        return (None, None, None, *prog.flat.grad_views())
+        return (None, None, None, None, *prog.flat.grad_views())
 
 
 class STFLSTMUNet(nn.Module):
@@ -822,4 +821,13 @@ class STFLSTMUNet(nn.Module):
         prog = self.program
         prog.check_device_errors(x.device)       # step boundary: an earlier step's LSTM timeout raises
         prog.flat.ensure()
-        return {"out": _STFFunction.apply(x, prog, _lib.storage_for(self.storage_dtype), *prog.flat.params)}
+        grad = torch.is_grad_enabled()
+        if grad and x.requires_grad:
+            raise NotImplementedError("stfunet.STFLSTMUNet computes parameter gradients only; the input "
+                                      "sequence must not require grad")
+        params = prog.flat.params
+        need_bwd = grad and prog.flat.any_requires_grad()
+        storage = _lib.storage_for(self.storage_dtype)
+        with _lib.storage(storage), torch.no_grad():    # (as inside autograd.Function.forward)
+            res = prog.runtime.forward(x, self.training, need_bwd)      # launched before autograd's bookkeeping
+        return {"out": _STFFunction.apply(x, prog, storage, res, *params)}

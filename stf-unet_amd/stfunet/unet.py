@@ -273,18 +273,22 @@ class UNetProgram:
 
 
 class _UNetFunction(torch.autograd.Function):
+    """``res``: (logits, saved state) of the plan-cached forward UNet.forward already enqueued (the
+    GPU starts while autograd processes the parameter inputs), or None (input gradients: the eager
+    forward runs here)."""
     @staticmethod
-    def forward(ctx, x, prog, storage, *params):
+    def forward(ctx, x, prog, storage, res, *params):
         ctx.need_dx = ctx.needs_input_grad[0]
         if ctx.need_dx and prog.m.in_channels % 8:
             raise NotImplementedError("input gradients need in_channels % 8 == 0 (the input is not "
                                       "channel-padded then)")
-        need_bwd = any(ctx.needs_input_grad[3:]) or ctx.need_dx
-        with _lib.storage(storage):
-            if ctx.need_dx:
+        if res is not None:
+            logits, saved = res
+            prog.runtime.own(saved, ctx)
+        else:
+            need_bwd = any(ctx.needs_input_grad[4:]) or ctx.need_dx
+            with _lib.storage(storage):
                 logits, saved = prog.forward(x, prog.m.training, need_bwd)
-            else:
-                logits, saved = prog.runtime.forward(x, prog.m.training, need_bwd, ctx)
         ctx.storage = storage
         ctx.prog = prog
         ctx.saved = saved
@@ -305,7 +309,7 @@ class _UNetFunction(torch.autograd.Function):
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0, ())
         dx, prog.dx = prog.dx, None
-        return (dx, None, None, *prog.flat.grad_views())
+        return (dx, None, None, None, *prog.flat.grad_views())
 
 
 class UNet(nn.Module):
@@ -346,4 +350,11 @@ class UNet(nn.Module):
                                "to a ROCm device (no CPU fallback)")
         prog = self.program
         prog.flat.ensure()
-        return {"out": _UNetFunction.apply(x, prog, _lib.storage_for(self.storage_dtype), *prog.flat.params)}
+        storage = _lib.storage_for(self.storage_dtype)
+        grad = torch.is_grad_enabled()
+        res = None
+        if not (grad and x.requires_grad):
+            need_bwd = grad and prog.flat.any_requires_grad()
+            with _lib.storage(storage), torch.no_grad():   # (as inside autograd.Function.forward)
+                res = prog.runtime.forward(x, self.training, need_bwd)   # launched before autograd's bookkeeping
+        return {"out": _UNetFunction.apply(x, prog, storage, res, *prog.flat.params)}
