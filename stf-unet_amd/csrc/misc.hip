@@ -142,6 +142,7 @@ STF_DEV int pack_tiles(const stf_pack_desc& d) {
                             : ((d.d0 + PK_IA - 1) / PK_IA) * ((bext + PK_IB - 1) / PK_IB);
 }
 
+constexpr int PK_UNR = 4;
 __global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __restrict__ descs) {
   __shared__ float tile[PK_TA * (PK_TB * PK_MAXRS + 1)];
   const stf_pack_desc d = descs[blockIdx.y];
@@ -152,9 +153,24 @@ __global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __r
     const int nbb = (d.d1 + PK_TB - 1) / PK_TB;
     const int a0 = (blockIdx.x / nbb) * PK_TA, b0 = (blockIdx.x % nbb) * PK_TB;
     const int na = min(PK_TA, d.d0 - a0), nb = min(PK_TB, d.d1 - b0), cols = nb * RS, LS = PK_TB * PK_MAXRS + 1;
-    for (int e = tid; e < na * cols; e += NT) {                // whole source rows: [a][b0..b0+nb)[tap]
-      const int a = e / cols, c = e - a * cols;
-      tile[a * LS + c] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+    // whole source rows [a][b0..b0+nb)[tap]; PK_UNR independent loads in flight per thread (one
+    // at a time, the loop waited on every load's latency: 1.6 TB/s)
+    for (int e0 = tid; e0 < na * cols; e0 += PK_UNR * NT) {
+      float v[PK_UNR];
+      int at[PK_UNR];
+#pragma unroll
+      for (int k = 0; k < PK_UNR; ++k) {
+        const int e = e0 + k * NT;
+        at[k] = -1;
+        if (e < na * cols) {
+          const int a = e / cols, c = e - a * cols;
+          v[k] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+          at[k] = a * LS + c;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PK_UNR; ++k)
+        if (at[k] >= 0) tile[at[k]] = v[k];
     }
     __syncthreads();
     const int qn = (na + 7) / 8;                               // 8-element chunks along a
@@ -174,9 +190,22 @@ __global__ __launch_bounds__(NT) void pack_tiled_kernel(const stf_pack_desc* __r
     const int a0 = (blockIdx.x / nbb) * PK_IA, b0 = (blockIdx.x % nbb) * PK_IB;
     const int na = min(PK_IA, d.d0 - a0), nb = min(PK_IB, bext - b0), LS = PK_IB * PK_MAXRS + 1;
     const int nbs = max(0, min(nb, d.d1 - b0));                // source columns present
-    for (int e = tid; e < na * nbs * RS; e += NT) {
-      const int a = e / (nbs * RS), c = e - a * nbs * RS;
-      tile[a * LS + c] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+    for (int e0 = tid; e0 < na * nbs * RS; e0 += PK_UNR * NT) {
+      float v[PK_UNR];
+      int at[PK_UNR];
+#pragma unroll
+      for (int k = 0; k < PK_UNR; ++k) {
+        const int e = e0 + k * NT;
+        at[k] = -1;
+        if (e < na * nbs * RS) {
+          const int a = e / (nbs * RS), c = e - a * nbs * RS;
+          v[k] = d.w[((long)(a0 + a) * d.d1 + b0) * RS + c];
+          at[k] = a * LS + c;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PK_UNR; ++k)
+        if (at[k] >= 0) tile[at[k]] = v[k];
     }
     __syncthreads();
     const int qn = (nb + 7) / 8;
