@@ -340,6 +340,14 @@ int stf_pack_sequence(const float* x, int B, int Ttot, int C, int H, int W, int 
  * zero padded; the stem conv is then a 1x1 GEMM over Kpad >= (C+P)*KS*KS columns. */
 int stf_stem_im2col(const float* x, int B, int Ttot, int C, int H, int W, int T, int P, int KS,
                     int stride, int pad, int Kpad, void* out, stf_stream_t stream);
+/* The same stem conv without the im2col tensor (ABI v15): x [B][Ttot][1][H][W] fp32 (frames 0..T-1,
+ * no PK maps) -> y NHWC bf16 [T*B][Ho][Wo][64] (Ho = (H-1)/2+1), w = the 64 x 64 bf16 rows the GEMM
+ * path packs (column k = r*7 + s, zero for k >= 49).  Bit-identical outputs to the im2col + 1x1 GEMM.
+ * stats (NULL: none): BatchNorm partial rows [T][grid][2][64] (sum, sum of squares of the stored
+ * bf16 values; grid = stf_stem_conv7_grid(B, T, H, W) rows per time step) for stf_bn_finalize. */
+int stf_stem_conv7_grid(int B, int T, int H, int W);
+int stf_stem_conv7(const float* x, int B, int Ttot, int H, int W, int T, const void* w, void* y, float* stats,
+                   stf_stream_t stream);
 /* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16.
  * argmax (uint8 [N][Ho][Wo][C], NULL in eval) records each window's first maximum
  * (index dy*3+dx, torch's tie rule); backward gathers dout over the <= 4 windows

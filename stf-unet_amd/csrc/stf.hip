@@ -404,6 +404,180 @@ __global__ void bilinear_ac_bwd_kernel(const uint16_t* __restrict__ dy, int N, i
   }
 }
 
+
+// Direct 7x7 / stride 2 / pad 3 stem convolution of a 1-channel frame sequence (ResNet-34 conv1,
+// src/stf_lstm_unet.py:108,177) into NHWC bf16 [T*B][Ho][Wo][64], with the grouped BatchNorm
+// statistics rows of its output -- the im2col + 1x1 GEMM path without the 268 MB im2col tensor
+// written and read back (cfg3).  A persistent workgroup walks 16 x 16 output tiles; per tile the
+// (2*16+5)^2 input patch (bf16, as the im2col rounds it) sits in LDS and every MFMA B fragment
+// (8 k-slots = 8 taps of one output pixel) is gathered from it; the 64 x 64 weights (k = r*7 + s,
+// zero past 49) stay in registers.  Same k order and MFMA sequence as the GEMM over the im2col
+// columns; output, epilogue and statistics rows as conv3x3_c8_kernel.
+constexpr int ST_T = 16, ST_P = 2 * ST_T + 5, ST_PR = ST_P * ST_P;   // 37 x 37 patch
+constexpr int ST_LD = (ST_PR + 255) / 256;                             // patch values per thread
+__global__ __launch_bounds__(256, 2) void stem7_conv_kernel(const float* __restrict__ x, int B, int Ttot, int H,
+                                                            int W, int T, int Ho, int Wo,
+                                                            const uint16_t* __restrict__ wgt,
+                                                            uint16_t* __restrict__ y, float* __restrict__ stats,
+                                                            int TY, int TX, int per, int rem) {
+  __shared__ uint16_t patch[2][ST_PR];
+  __shared__ float red[4][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int tpi = TY * TX, N = T * B;
+  const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
+  const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  e16x8 wf[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = (j >> 1) * 32 + (fr >> 2) * 8 + (j & 1) * 4 + (fr & 3);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) wf[j][ks] = *reinterpret_cast<const e16x8*>(wgt + (size_t)n * 64 + ks * 32 + fk * 8);
+  }
+  // this lane's 8 k-slots per k-step: tap offsets r * 37 + s in the patch (-1: zero column)
+  int toff[2][8];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = ks * 32 + fk * 8 + e;
+      toff[ks][e] = k < 49 ? (k / 7) * ST_P + k % 7 : -1;
+    }
+  if (stats && tid < 128) {
+    for (int g = 0; g < T; ++g) stats[((size_t)(g * gridDim.x + blockIdx.x) * 2 + (tid >> 6)) * 64 + (tid & 63)] = 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t rs_dst =
+      __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, (uint32_t)((size_t)N * Ho * Wo * 64 * 2), 0x00020000);
+  float ld[ST_LD];
+  auto load = [&](int tile) {
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    const int t = img / B, b = img - t * B;
+    const float* plane = x + ((size_t)b * Ttot + t) * H * W;
+#pragma unroll
+    for (int q = 0; q < ST_LD; ++q) {
+      const int e = tid + q * 256, py = e / ST_P, px = e - py * ST_P;
+      const int iy = ty * 2 * ST_T - 3 + py, ix = tx * 2 * ST_T - 3 + px;
+      ld[q] = (e < ST_PR && iy >= 0 && ix >= 0 && iy < H && ix < W) ? plane[(size_t)iy * W + ix] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < ST_LD; ++q)
+      if (tid + q * 256 < ST_PR) patch[buf][tid + q * 256] = __builtin_bit_cast(uint16_t, f2e(ld[q]));
+  };
+  float s1[2][8], s2[2][8];
+  auto zero_sums = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[h][e] = 0.f; s2[h][e] = 0.f; }
+  };
+  int run_key = -1;
+  auto flush = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[h][e] += __shfl_xor(s1[h][e], o, 64);
+          s2[h][e] += __shfl_xor(s2[h][e], o, 64);
+        }
+    if (fr == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wave][0][h * 32 + fk * 8 + e] = s1[h][e];
+          red[wave][1][h * 32 + fk * 8 + e] = s2[h][e];
+        }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int q = tid >> 6, c = tid & 63;
+      stats[((size_t)(run_key * gridDim.x + blockIdx.x) * 2 + q) * 64 + c] =
+          red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+    }
+    __syncthreads();
+    zero_sums();
+  };
+  zero_sums();
+  if (cnt > 0) { load(t0); store(0); }
+  __syncthreads();
+  for (int kk = 0; kk < cnt; ++kk) {
+    const int tile = t0 + kk, buf = kk & 1;
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    if (kk + 1 < cnt) load(tile + 1);
+    const int key = img / B;                             // statistics group = time step
+    if (stats && key != run_key) {
+      if (run_key >= 0) flush();
+      run_key = key;
+    }
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      e16x8 xf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int base = 2 * (wave * 4 + i) * ST_P + 2 * fr;   // output pixel (row wave*4+i, column fr)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          xf[i][e] = toff[ks][e] >= 0 ? __builtin_bit_cast(e16, patch[buf][base + toff[ks][e]]) : e16(0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(wf[j][ks], xf[i], acc[i][j]);
+    }
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oy = ty * ST_T + wave * 4 + i, ox = tx * ST_T + fr;
+      const bool ok = oy < Ho && ox < Wo;
+      const size_t m = ((size_t)img * Ho + oy) * Wo + ox;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = round_e(acc[i][2 * h][r]);
+          f[4 + r] = round_e(acc[i][2 * h + 1][r]);
+        }
+        const uint4 u = pack8(f);
+        const uint32_t off = ok ? (uint32_t)((m * 64 + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        if (ok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[h][e] += f[e]; s2[h][e] += f[e] * f[e]; }
+        }
+      }
+    }
+    if (kk + 1 < cnt) store(buf ^ 1);
+    __syncthreads();
+  }
+  if (stats && run_key >= 0) flush();
+}
+
+int stem7_tiles(int N, int Ho, int Wo, int& TY, int& TX) {
+  TY = (Ho + ST_T - 1) / ST_T;
+  TX = (Wo + ST_T - 1) / ST_T;
+  return N * TY * TX;
+}
+
+int stem7_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
 }  // namespace
 
 extern "C" int stf_bilinear_ac_fwd(const void* x, int N, int H, int W, int C, int x_cstride, void* y, int h, int w,
@@ -526,6 +700,29 @@ extern "C" int stf_pk_resize(const float* x, int B, int Ttot, int T, int P, int 
   const long total = (long)T * B * h * w * P;
   hipLaunchKernelGGL(pk_resize_kernel, dim3(grid_for(total, 8192)), dim3(NT), 0, (hipStream_t)stream, x, B, Ttot,
                      T, P, H, W, h, w, (uint16_t*)dst, dst_cstride, coff);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_stem_conv7_grid(int B, int T, int H, int W) {
+  if (B < 1 || T < 1 || H < 1 || W < 1) return 0;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  int TY, TX;
+  const int tiles = stem7_tiles(T * B, Ho, Wo, TY, TX);
+  return std::min(tiles, 2 * stem7_cus());
+}
+
+extern "C" int stf_stem_conv7(const float* x, int B, int Ttot, int H, int W, int T, const void* wgt, void* y,
+                              float* stats, stf_stream_t stream) {
+  if (!x || !wgt || !y || B < 1 || T < 1 || Ttot < T || H < 1 || W < 1) return STF_EINVAL;
+  if (((uintptr_t)wgt & 15) || ((uintptr_t)y & 15)) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  if ((size_t)T * B * Ho * Wo * 64 * 2 >= 0xFFFFFF00ull) return STF_EINVAL;    // 32-bit store offsets
+  int TY, TX;
+  const int tiles = stem7_tiles(T * B, Ho, Wo, TY, TX);
+  const int grid = stf_stem_conv7_grid(B, T, H, W);
+  hipLaunchKernelGGL(stem7_conv_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, B, Ttot, H, W, T, Ho, Wo,
+                     (const uint16_t*)wgt, (uint16_t*)y, stats, TY, TX, tiles / grid, tiles % grid);
   STF_CHECK_LAUNCH();
   return 0;
 }

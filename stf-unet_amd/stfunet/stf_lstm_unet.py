@@ -496,6 +496,18 @@ class STFProgram:
             call("stf_pack_sequence", _p(x), B, Ttot, Cf, H, W, T, P, 8, xin.ptr(), stream())
             stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1, 0, 8), 64, y0, 7, 7, 2, 3,
                                       want_stats=training, groups=T)
+        elif kreal == 49 and _STEM_DIRECT:
+            # one frame channel: the direct 7x7/s2 kernel (no im2col tensor: 268 MB written and read
+            # back at cfg3); the weight gradient's im2col columns are formed in the backward on a
+            # side stream (S.xin = None until then)
+            xin = None
+            wp = nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, 64)
+            tiles = _lib.load().stf_stem_conv7_grid(B, T, H, W)
+            stats = nhwc.empty(T * tiles * 2 * 64, torch.float32, dev) if training else None
+            call("stf_stem_conv7", _p(x), B, Ttot, H, W, T, _p(wp), y0.ptr(), _p(stats), stream())
+            if not training:
+                tiles = 0
+            S.x = x
         else:
             kpad = 64 if kreal <= 64 else (kreal + 31) // 32 * 32
             xin = new_feat(N, h2, w2, kpad, dev)
@@ -636,6 +648,15 @@ class STFProgram:
         # side stream as soon as its h_T gradient (the decoder's skip slice) is final
         side = self.side_streams(dev)
         main = torch.cuda.current_stream(dev)
+        if S.xin is None and not S.stem_gather:
+            # direct stem conv: the im2col columns of the stem's weight gradient, on lstm 1's side
+            # stream ahead of its backward -- the main stream waits for that stream before encoder
+            # layer 1's first block, long before the stem weight gradient reads them
+            with torch.cuda.stream(side[0]):
+                S.xin = new_feat(S.y0.N, S.y0.H, S.y0.W, 64, dev)
+                call("stf_stem_im2col", _p(S.x), B, S.x.shape[1], S.x.shape[2], S.H, S.W, T, P, 7, 2, 3, 64,
+                     S.xin.ptr(), stream())
+            S.xin.buf.record_stream(main)
         dhT = [None] * 4
         de = [None] * 4
 
@@ -730,6 +751,9 @@ class STFProgram:
         nhwc.copy_rows(fus.weight.detach(), cin, w, pkb.C, C, cin)
         nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0)
         return dpk.slice(0, C)
+
+
+_STEM_DIRECT = os.environ.get("STF_STEM_DIRECT", "1") != "0"     # (A/B: 0 = im2col + 1x1 GEMM)
 
 
 def _check_input_shape(shape, P):

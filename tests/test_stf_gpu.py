@@ -820,3 +820,31 @@ def test_stf_training_steps_repeatable(monkeypatch):
     assert torch.isfinite(la).all()
     assert torch.equal(la, lb), (la, lb)
     assert torch.equal(pa, pb)
+
+
+@pytest.mark.parametrize("B, T, H, W", [(2, 3, 64, 80), (1, 2, 37, 50)])
+def test_stem_conv7_direct_equals_im2col_gemm(B, T, H, W):
+    """The direct 7x7/s2 stem kernel (stf_stem_conv7) against the im2col + 1x1 GEMM path it replaces
+    (src/stf_lstm_unet.py:108,177): the bf16 output bit for bit (same k order and MFMA sequence), the
+    per-time-step BatchNorm sums of its statistics rows to fp32 rounding; odd sizes hit partial tiles
+    and the zero padding."""
+    from stfunet import _lib, nhwc
+    from stfunet._lib import call
+    torch.manual_seed(5)
+    x = torch.randn(B, T + 1, 1, H, W, device="cuda")          # one extra frame the stem must skip
+    w1 = torch.randn(64, 1, 7, 7, device="cuda") * 0.1
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    wp = nhwc.pack_weight(w1.view(64, -1, 1, 1), 0, 64)
+    xin = nhwc.new_feat(T * B, Ho, Wo, 64, "cuda")
+    call("stf_stem_im2col", x.data_ptr(), B, T + 1, 1, H, W, T, 0, 7, 2, 3, 64, xin.ptr(), _lib.stream())
+    y_ref = nhwc.new_feat(T * B, Ho, Wo, 64, "cuda")
+    st_ref, tiles_ref = nhwc.igemm(xin, wp, 64, y_ref, 1, 1, 1, 0, want_stats=True, groups=T)
+    y = nhwc.new_feat(T * B, Ho, Wo, 64, "cuda")
+    tiles = _lib.load().stf_stem_conv7_grid(B, T, H, W)
+    st = torch.empty(T * tiles * 2 * 64, dtype=torch.float32, device="cuda")
+    call("stf_stem_conv7", x.data_ptr(), B, T + 1, H, W, T, wp.data_ptr(), y.ptr(), st.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y.buf, y_ref.buf)
+    s_new = st.view(T, tiles, 2, 64).double().sum(1)
+    s_ref = st_ref.view(T, tiles_ref, 2, 64).double().sum(1)
+    assert torch.allclose(s_new, s_ref, rtol=1e-5, atol=1e-3)
