@@ -348,6 +348,11 @@ int stf_stem_im2col(const float* x, int B, int Ttot, int C, int H, int W, int T,
 int stf_stem_conv7_grid(int B, int T, int H, int W);
 int stf_stem_conv7(const float* x, int B, int Ttot, int H, int W, int T, const void* w, void* y, float* stats,
                    stf_stream_t stream);
+/* Its weight gradient without the im2col tensor: dy NHWC bf16 [T*B][Ho][Wo][64] (the stem output's
+ * gradient) -> fp32 partial slabs ws [grid][64][64] (dy channel x column k = r*7 + s; columns >= 49
+ * zero; grid = stf_stem_conv7_grid(...)), folded with stf_wgrad_reduce(ws, grid, 64, 1, 1, 64, ..). */
+int stf_stem_wgrad7(const float* x, int B, int Ttot, int H, int W, int T, const void* dy, float* ws,
+                    stf_stream_t stream);
 /* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16.
  * argmax (uint8 [N][Ho][Wo][C], NULL in eval) records each window's first maximum
  * (index dy*3+dx, torch's tie rule); backward gathers dout over the <= 4 windows

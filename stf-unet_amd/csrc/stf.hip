@@ -562,6 +562,91 @@ __global__ __launch_bounds__(256, 2) void stem7_conv_kernel(const float* __restr
   if (stats && run_key >= 0) flush();
 }
 
+// The stem's weight gradient without the im2col tensor: dW[n][k] = sum over output pixels of
+// dy[px][n] * patch(px, tap k), per 16 x 16 output tile the dy tile [256 px][64] and the 37 x 37
+// input patch in LDS, both MFMA operands gathered from them (k = pixel).  Wave w owns dy channels
+// 16w..16w+15 x all 64 taps (49 real); every workgroup writes its fp32 partial [64][64] slab
+// (ws[blockIdx.x]), stf_wgrad_reduce folds them in order.
+__global__ __launch_bounds__(256, 2) void stem7_wgrad_kernel(const float* __restrict__ x, int B, int Ttot, int H,
+                                                             int W, int T, int Ho, int Wo,
+                                                             const uint16_t* __restrict__ dy, float* __restrict__ ws,
+                                                             int TY, int TX, int per, int rem) {
+  __shared__ uint16_t patch[2][ST_PR];
+  __shared__ __attribute__((aligned(16))) uint16_t dyt[2][256 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int tpi = TY * TX;
+  const int cnt = per + (int)(blockIdx.x < (unsigned)rem);
+  const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  int toff[4];                                           // this lane's tap (kb * 16 + fr) in the patch
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    const int k = kb * 16 + fr;
+    toff[kb] = k < 49 ? (k / 7) * ST_P + k % 7 : -1;
+  }
+  float ld[ST_LD];
+  uint4 dv[8];
+  auto load = [&](int tile) {
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    const int t = img / B, b = img - t * B;
+    const float* plane = x + ((size_t)b * Ttot + t) * H * W;
+#pragma unroll
+    for (int q = 0; q < ST_LD; ++q) {
+      const int e = tid + q * 256, py = e / ST_P, px = e - py * ST_P;
+      const int iy = ty * 2 * ST_T - 3 + py, ix = tx * 2 * ST_T - 3 + px;
+      ld[q] = (e < ST_PR && iy >= 0 && ix >= 0 && iy < H && ix < W) ? plane[(size_t)iy * W + ix] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + q * 256, p = e >> 3, c8 = e & 7;
+      const int oy = ty * ST_T + (p >> 4), ox = tx * ST_T + (p & 15);
+      dv[q] = make_uint4(0, 0, 0, 0);
+      if (oy < Ho && ox < Wo) dv[q] = *reinterpret_cast<const uint4*>(dy + (((size_t)img * Ho + oy) * Wo + ox) * 64 + c8 * 8);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < ST_LD; ++q)
+      if (tid + q * 256 < ST_PR) patch[buf][tid + q * 256] = __builtin_bit_cast(uint16_t, f2e(ld[q]));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) *reinterpret_cast<uint4*>(&dyt[buf][(tid + q * 256) * 8]) = dv[q];
+  };
+  f32x4 acc[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) acc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (cnt > 0) { load(t0); store(0); }
+  __syncthreads();
+  for (int kk = 0; kk < cnt; ++kk) {
+    const int buf = kk & 1;
+    if (kk + 1 < cnt) load(t0 + kk + 1);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      // k-slots fk*8+e = pixels ks*32 + fk*8 + e: one 8-pixel run of output row (ks*32 + fk*8) / 16
+      const int p0 = ks * 32 + fk * 8;
+      const int pb = 2 * (p0 >> 4) * ST_P + 2 * (p0 & 15);
+      e16x8 a;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = __builtin_bit_cast(e16, dyt[buf][(p0 + e) * 64 + wave * 16 + fr]);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        e16x8 bq;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          bq[e] = toff[kb] >= 0 ? __builtin_bit_cast(e16, patch[buf][pb + 2 * e + toff[kb]]) : e16(0.f);
+        acc[kb] = mfma16x16x32(a, bq, acc[kb]);
+      }
+    }
+    if (kk + 1 < cnt) store(buf ^ 1);
+    __syncthreads();
+  }
+  // lane (fr, fk), element r: dy channel wave*16 + 4*fk + r, tap kb*16 + fr
+  float* slab = ws + (size_t)blockIdx.x * 64 * 64;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[(wave * 16 + 4 * fk + r) * 64 + kb * 16 + fr] = acc[kb][r];
+}
+
 int stem7_tiles(int N, int Ho, int Wo, int& TY, int& TX) {
   TY = (Ho + ST_T - 1) / ST_T;
   TX = (Wo + ST_T - 1) / ST_T;
@@ -723,6 +808,20 @@ extern "C" int stf_stem_conv7(const float* x, int B, int Ttot, int H, int W, int
   const int grid = stf_stem_conv7_grid(B, T, H, W);
   hipLaunchKernelGGL(stem7_conv_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, B, Ttot, H, W, T, Ho, Wo,
                      (const uint16_t*)wgt, (uint16_t*)y, stats, TY, TX, tiles / grid, tiles % grid);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_stem_wgrad7(const float* x, int B, int Ttot, int H, int W, int T, const void* dy, float* ws,
+                               stf_stream_t stream) {
+  if (!x || !dy || !ws || B < 1 || T < 1 || Ttot < T || H < 1 || W < 1) return STF_EINVAL;
+  if (((uintptr_t)dy & 15) || ((uintptr_t)ws & 15)) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  int TY, TX;
+  const int tiles = stem7_tiles(T * B, Ho, Wo, TY, TX);
+  const int grid = stf_stem_conv7_grid(B, T, H, W);
+  hipLaunchKernelGGL(stem7_wgrad_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, B, Ttot, H, W, T, Ho, Wo,
+                     (const uint16_t*)dy, ws, TY, TX, tiles / grid, tiles % grid);
   STF_CHECK_LAUNCH();
   return 0;
 }

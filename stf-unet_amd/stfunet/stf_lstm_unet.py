@@ -498,8 +498,7 @@ class STFProgram:
                                       want_stats=training, groups=T)
         elif kreal == 49 and _STEM_DIRECT:
             # one frame channel: the direct 7x7/s2 kernel (no im2col tensor: 268 MB written and read
-            # back at cfg3); the weight gradient's im2col columns are formed in the backward on a
-            # side stream (S.xin = None until then)
+            # back at cfg3), and in the backward its weight gradient straight from the frames too
             xin = None
             wp = nhwc.pack_weight(w1.view(w1.shape[0], -1, 1, 1), 0, 64)
             tiles = _lib.load().stf_stem_conv7_grid(B, T, H, W)
@@ -648,15 +647,7 @@ class STFProgram:
         # side stream as soon as its h_T gradient (the decoder's skip slice) is final
         side = self.side_streams(dev)
         main = torch.cuda.current_stream(dev)
-        if S.xin is None and not S.stem_gather:
-            # direct stem conv: the im2col columns of the stem's weight gradient, on lstm 1's side
-            # stream ahead of its backward -- the main stream waits for that stream before encoder
-            # layer 1's first block, long before the stem weight gradient reads them
-            with torch.cuda.stream(side[0]):
-                S.xin = new_feat(S.y0.N, S.y0.H, S.y0.W, 64, dev)
-                call("stf_stem_im2col", _p(S.x), B, S.x.shape[1], S.x.shape[2], S.H, S.W, T, P, 7, 2, 3, 64,
-                     S.xin.ptr(), stream())
-            S.xin.buf.record_stream(main)
+
         dhT = [None] * 4
         de = [None] * 4
 
@@ -726,7 +717,16 @@ class STFProgram:
         dy0 = nhwc.bn_backward_maxpool3(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), S.pool_arg, dout)
         w1 = m.conv1.weight
         kreal = w1[0].numel()
-        if S.stem_gather:                      # 8-channel packed input, 7x7/s2 gather
+        if S.xin is None:                      # direct stem conv: the gradient gathers the input too
+            assert dy0.cs == 64 and dy0.off == 0
+            lib = _lib.load()
+            grid = lib.stf_stem_conv7_grid(B, T, S.H, S.W)
+            ws = nhwc.empty(grid * 64 * 64, torch.float32, dev)
+            call("stf_stem_wgrad7", _p(S.x), B, S.x.shape[1], S.H, S.W, T, dy0.ptr(), _p(ws), stream())
+            tmp = nhwc.empty(64 * 64, torch.float32, dev)
+            call("stf_wgrad_reduce", _p(ws), grid, 64, 1, 1, 64, _p(tmp), stream())
+            nhwc.copy_rows(tmp, 64, gv(w1), kreal, w1.shape[0], kreal)
+        elif S.stem_gather:                    # 8-channel packed input, 7x7/s2 gather
             tmp = nhwc.empty(w1.shape[0] * 8 * 49, torch.float32, dev)
             nhwc.wgrad(dy0, S.xin, 7, 7, 2, 3, tmp, defer=False)
             nhwc.copy_rows(tmp, 8 * 49, gv(w1), w1.shape[1] * 49, w1.shape[0], w1.shape[1] * 49)

@@ -848,3 +848,18 @@ def test_stem_conv7_direct_equals_im2col_gemm(B, T, H, W):
     s_new = st.view(T, tiles, 2, 64).double().sum(1)
     s_ref = st_ref.view(T, tiles_ref, 2, 64).double().sum(1)
     assert torch.allclose(s_new, s_ref, rtol=1e-5, atol=1e-3)
+    # the weight gradient from the frames (stf_stem_wgrad7 + reduce) against the GEMM wgrad over the
+    # im2col columns, with a random output gradient
+    dy = nhwc.new_feat(T * B, Ho, Wo, 64, "cuda")
+    dy.buf.copy_(torch.randn(dy.buf.numel(), device="cuda").to(dy.buf.dtype))
+    ref = torch.empty(64 * 64, dtype=torch.float32, device="cuda")
+    nhwc.wgrad(dy, xin, 1, 1, 1, 0, ref, defer=False)
+    ws = torch.empty(tiles * 64 * 64, dtype=torch.float32, device="cuda")
+    call("stf_stem_wgrad7", x.data_ptr(), B, T + 1, H, W, T, dy.ptr(), ws.data_ptr(), _lib.stream())
+    got = torch.empty(64 * 64, dtype=torch.float32, device="cuda")
+    call("stf_wgrad_reduce", ws.data_ptr(), tiles, 64, 1, 1, 64, got.data_ptr(), _lib.stream())
+    torch.cuda.synchronize()
+    ref, got = ref.view(64, 64), got.view(64, 64)
+    assert torch.count_nonzero(got[:, 49:]) == 0
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-4 * ref.abs().max().item() + 1e-3, err
