@@ -766,7 +766,12 @@ void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
   const long rsc = (long)a->g.R * a->g.S * a->g.Cs;
   const long cblocks = (a->g.Cs % 64 && rsc > 64 && rsc <= 96) ? 1 : (rsc + bm - 1) / bm;
   const long tiles = (long)((a->Nout + bm - 1) / bm) * cblocks;
-  long want = (2048 + tiles - 1) / tiles;
+  // K splits until ~target workgroups: every split writes a [Nout][R*S*Cs] fp32 slab that the reduce
+  // reads back, so the 128 x 128 tile (1x1 weight gradients of the STF LSTMs and downsamples: up to
+  // 1024 splits of 134 MB slabs at 2048) aims at two workgroups per CU (STF cfg3 +2.6 % over 2048,
+  // same box); the 64-wide tiles keep 2048 (UNet's first layer: 512 measured -0.5..-0.8 %)
+  const long target = big_tile(a) ? 512 : 2048;
+  long want = (target + tiles - 1) / tiles;
   long maxs = (M + 4 * bkp - 1) / (4 * bkp);        // at least 4 K steps per split
   if (want > maxs) want = maxs;
   if (want < 1) want = 1;
