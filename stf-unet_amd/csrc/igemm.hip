@@ -2061,12 +2061,16 @@ long halo_items_ix(const stf_igemm_args* a, int ix) {
   return (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
 }
 
-// stages of the 8 x 8 (IX = 4) halo kernel: the single-stage kernel relies on two workgroups per
-// CU, so with fewer items than 2 x CUs the 2-stage ring runs instead (STF_HALO4_ST=1 / 2 forces one)
+// stages of the 8 x 8 (IX = 4) halo kernel (STF_HALO4_ST=2: the 2-stage ring).  With fewer items
+// than 2 x CUs (STF cfg3: 256) the single-stage kernel runs one workgroup per CU with its DMA waits
+// exposed, and the 2-stage ring is faster alone (census: forward 64 -> 61 us, BN-backward dgrad
+// 84 -> 66 us) -- but in the step, beside the side streams' weight gradients and LSTMs that its
+// 123 KB of LDS keeps off the CU, it measured -0.5 % on average over five same-box repeats, so
+// the single-stage kernel stays the default
 int halo4_stages(const stf_igemm_args* a) {
-  static const int force = stf::ab_switch("STF_HALO4_ST", 0);
-  if (force == 1 || force == 2) return force;
-  return halo_items_ix(a, 4) < 2L * num_cus() ? 2 : 1;
+  static const int force = stf::ab_switch("STF_HALO4_ST", 1);
+  (void)a;
+  return force == 2 ? 2 : 1;
 }
 
 // persistent halo grid: one workgroup per CU (160 KiB LDS each; the single-stage 8 x 8 kernel two)
