@@ -496,7 +496,7 @@ class STFProgram:
             call("stf_pack_sequence", _p(x), B, Ttot, Cf, H, W, T, P, 8, xin.ptr(), stream())
             stats, tiles = nhwc.igemm(xin, nhwc.pack_weight(w1, 0, 8), 64, y0, 7, 7, 2, 3,
                                       want_stats=training, groups=T)
-        elif kreal == 49 and _STEM_DIRECT:
+        elif kreal == 49 and _STEM_DIRECT and N * h2 * w2 * 64 * 2 < 0xFFFFFF00:    # (32-bit store offsets)
             # one frame channel: the direct 7x7/s2 kernel (no im2col tensor: 268 MB written and read
             # back at cfg3), and in the backward its weight gradient straight from the frames too
             xin = None
