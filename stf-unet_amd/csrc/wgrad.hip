@@ -347,6 +347,139 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_kernel(WArgs a, int tiles_y, i
 }
 
 // ---------------------------------------------------------------------------
+// Fused-tap 3x3 weight gradient of the 8-channel-input layer (UNet's first conv, the input of
+// conv3x3_c8_kernel; src/unet.py:10-18): dW[n][tap*8 + c] = sum over pixels of dy[px][n] *
+// x[px + tap][c].  A persistent workgroup walks 16 x 16 pixel tiles with the dy tile [256 px][64]
+// and the 18 x 18 halo of 16-B x rows in LDS (each dy and x element read from HBM about once --
+// the generic kernel gathers x per tap); both MFMA operands are gathered from them (k = pixel).
+// Wave w owns tile rows 4w..4w+3 (64 pixels of the K sum) x all 64 dy channels x the 72 columns
+// (4 x 5 blocks of 16; the last block's upper half duplicates tap 8 and is dropped) -- splitting K
+// instead of the channels keeps the x reads unshared.  Both operands come out of their row-major
+// LDS images already K-major through ds_read_b64_tr_b16 (a 16-lane group reads 4 pixel rows x 16
+// columns and lane i receives column i), two reads per 8-pixel fragment: 18 LDS reads per 32
+// pixels where per-element gathers take 72.  The 4 wave partials are added through LDS at the end
+// and every workgroup writes its fp32 slab [64][72] (split = blockIdx.x), stf_wgrad_reduce folds
+// them.
+constexpr int WC8_T = 16, WC8_HW = WC8_T + 2, WC8_HR = WC8_HW * WC8_HW;
+// halo row stride 22 pixels: the taps 2 and 3 (read by one transposed read) then sit 20 rows =
+// 4 (mod 8) bank slots apart, conflict-free with the neighbouring 8-pixel group
+constexpr int WC8_HL = 22, WC8_HBYTES = WC8_HW * WC8_HL * 16;
+constexpr int WC8_STAGE = WC8_HBYTES + 256 * 64 * 2;     // bytes: halo rows + dy tile
+// dy tile: 32-B slot h of pixel p stored at slot h ^ wc8_swz(p), so that the 8 pixel rows one
+// 32-lane half of a transposed read touches (p0 + 0..3, p0 + 8..11) cover all 64 banks once
+__device__ __forceinline__ int wc8_swz(int p) { return ((p >> 1) & 1) | (((p >> 3) & 1) << 1); }
+typedef short wc8_s4 __attribute__((ext_vector_type(4)));
+typedef short wc8_s8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ e16x8 wc8_tr(const uint8_t* p, int second) {
+  typedef __attribute__((address_space(3))) wc8_s4* lp;
+  const wc8_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p));
+  const wc8_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lp)(p + second));
+  return __builtin_bit_cast(e16x8, (wc8_s8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+__global__ __launch_bounds__(NT, 2) void wgrad3x3_c8_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * WC8_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4, q = fr >> 2, pq = fr & 3;
+  const int t_begin = blockIdx.x * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
+  const int per_img = tiles_y * tiles_x;
+  const int cnt = t_end - t_begin;
+  // transposed-read addresses (bytes from the stage base).  Lane 4q+pq of a 16-lane group supplies
+  // row q's columns 4pq..4pq+3.  A (dy): rows = pixels p0+q, columns = channels nb*16 + 4pq.
+  // B (x): rows = pixels p0+q shifted by a tap, columns = (tap pair of block kb)[pq>>1], channels
+  // 4*(pq&1)..+3; block 4's second tap duplicates tap 8 (its columns are dropped).
+  int aoff[2][4], boff[2][5];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int p0 = wave * 64 + ks * 32 + fk * 8, px = p0 + q;
+    const int hb = (p0 >> 4) * WC8_HL + (p0 & 15) + q;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+      aoff[ks][nb] = WC8_HBYTES + px * 128 + (((nb ^ wc8_swz(px)) * 2 + (pq >> 1)) << 4) + (pq & 1) * 8;
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) {
+      const int t = kb == 4 ? 8 : 2 * kb + (pq >> 1);
+      boff[ks][kb] = (hb + (t / 3) * WC8_HL + t % 3) * 16 + (pq & 1) * 8;
+    }
+  }
+  uint4 hv[2], dv[8];
+  auto load = [&](int t) {
+    const int img = t / per_img, rem = t - img * per_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2) {
+      const int hr = tid + q2 * 256, hy = hr / WC8_HW, hx = hr - hy * WC8_HW;
+      const int ys = ty * WC8_T - 1 + hy, xs = tx * WC8_T - 1 + hx;
+      hv[q2] = make_uint4(0, 0, 0, 0);
+      if (hr < WC8_HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws)
+        hv[q2] = *reinterpret_cast<const uint4*>(a.x + ((size_t)(img * a.Hs + ys) * a.Ws + xs) * a.xcs);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 8; ++q2) {
+      const int e = tid + q2 * 256, p = e >> 3, c8 = e & 7;
+      const int oy = ty * WC8_T + (p >> 4), ox = tx * WC8_T + (p & 15);
+      dv[q2] = make_uint4(0, 0, 0, 0);
+      if (oy < a.Hd && ox < a.Wd)
+        dv[q2] = *reinterpret_cast<const uint4*>(a.dy + ((size_t)(img * a.Hd + oy) * a.Wd + ox) * a.dycs + c8 * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    uint4* h = reinterpret_cast<uint4*>(lds + buf * WC8_STAGE);
+    uint4* d = reinterpret_cast<uint4*>(lds + buf * WC8_STAGE + WC8_HBYTES);
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2) {
+      const int hr = tid + q2 * 256, hy = hr / WC8_HW;
+      if (hr < WC8_HR) h[hy * WC8_HL + hr - hy * WC8_HW] = hv[q2];
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 8; ++q2) {
+      const int e = tid + q2 * 256, p = e >> 3, c8 = e & 7;
+      d[p * 8 + ((((c8 >> 1) ^ wc8_swz(p)) << 1) | (c8 & 1))] = dv[q2];
+    }
+  };
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb) acc[nb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (cnt > 0) { load(t_begin); store(0); }
+  __syncthreads();
+  for (int kk = 0; kk < cnt; ++kk) {
+    const int buf = kk & 1;
+    if (kk + 1 < cnt) load(t_begin + kk + 1);
+    const uint8_t* st = lds + buf * WC8_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // k-slots fk*8 + 0..7 = pixels p0 + 0..7 (p0 = wave*64 + ks*32 + fk*8) in both operands
+      e16x8 bq[5];
+#pragma unroll
+      for (int kb = 0; kb < 5; ++kb) bq[kb] = wc8_tr(st + boff[ks][kb], 4 * 16);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const e16x8 av = wc8_tr(st + aoff[ks][nb], 4 * 128);
+#pragma unroll
+        for (int kb = 0; kb < 5; ++kb) acc[nb][kb] = mfma16x16x32(av, bq[kb], acc[nb][kb]);
+      }
+    }
+    if (kk + 1 < cnt) store(buf ^ 1);
+    __syncthreads();
+  }
+  // lane (fr, fk), element r: dy channel nb*16 + 4*fk + r; column fr of block kb = tap
+  // (kb < 4 ? 2*kb + (fr >> 3) : 8), channel fr & 7 -> slab column tap*8 + channel (tap-major, as
+  // the other fused kernels' slabs); the 4 wave partials [64][72] meet in LDS
+  float* red = reinterpret_cast<float*>(lds);                  // [4][64][72] = 73.7 KB
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int kb = 0; kb < 5; ++kb)
+      if (kb < 4 || fr < 8)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(wave * 64 + nb * 16 + 4 * fk + r) * 72 + kb * 16 + fr] = acc[nb][kb][r];
+  __syncthreads();
+  float* slab = a.ws + (size_t)blockIdx.x * 64 * 72;
+  for (int i = tid; i < 64 * 72; i += NT)
+    slab[i] = (red[i] + red[64 * 72 + i]) + (red[2 * 64 * 72 + i] + red[3 * 64 * 72 + i]);
+}
+
+// ---------------------------------------------------------------------------
 // The same fused-tap weight gradient with LDS-DMA staging: dy tile and x halo go
 // global -> LDS by `buffer_load ... lds` (no register staging, no ds_write), in a
 // 3-stage ring with two tiles in flight.  Rows are 128 B (64 channels); the 16-B
@@ -741,6 +874,21 @@ int fused22_nb(const stf_wgrad_args* a) {
   return (a->Nout % 128 == 0 && a->Nout >= 256) ? 2 : 1;
 }
 
+// the 8-channel-input 3x3 layer (conv3x3_c8_kernel's weight gradient; STF_WGRAD_C8=0: the
+// generic wgrad_kernel<64, 96, 64, true>, A/B)
+bool fused_c8(const stf_wgrad_args* a) {
+  static const bool enabled = stf::ab_switch("STF_WGRAD_C8", 1) != 0;
+  const stf_conv_geom& c = a->g;
+  return enabled && c.R == 3 && c.S == 3 && c.stride == 1 && c.pad == 1 && c.Hd == c.Hs && c.Wd == c.Ws &&
+         c.Cs == 8 && c.src_cstride == 8 && a->Nout == 64 && !c.transposed;
+}
+
+void c8_tiles(const stf_wgrad_args* a, int& ty, int& tx, int& nt) {
+  ty = (a->g.Hd + WC8_T - 1) / WC8_T;
+  tx = (a->g.Wd + WC8_T - 1) / WC8_T;
+  nt = a->g.N * ty * tx;
+}
+
 void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
   ty = (a->g.Hd + 64 / pw - 1) / (64 / pw);
   tx = (a->g.Wd + pw - 1) / pw;
@@ -748,6 +896,14 @@ void fused_tiles(const stf_wgrad_args* a, int pw, int& ty, int& tx, int& nt) {
 }
 
 void plan(const stf_wgrad_args* a, int& splits, int& chunk) {
+  if (fused_c8(a)) {                                 // persistent: two workgroups per CU
+    int ty, tx, nt;
+    c8_tiles(a, ty, tx, nt);
+    const long want = std::min<long>(nt, a->grid_blocks > 0 ? a->grid_blocks : 512);
+    chunk = (int)((nt + want - 1) / want);
+    splits = (nt + chunk - 1) / chunk;
+    return;
+  }
   if (const int pw = fused_pw(a) ? fused_pw(a) : fused22_pw(a)) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);
@@ -790,6 +946,7 @@ extern "C" int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_b
 }
 
 extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
+  if (fused_c8(a)) return "wgrad3x3_c8_kernel";
   if (const int pw = fused_pw(a)) {
     if (wgrad_dma(a)) return pw == 16 ? "wgrad3x3_dma_kernel<16>" : "wgrad3x3_dma_kernel<8>";
     return pw == 16 ? "wgrad3x3_kernel<16, 0>" : "wgrad3x3_kernel<8, 0>";
@@ -823,6 +980,13 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
   w.one_slab = one_slab;
   hipStream_t s = (hipStream_t)stream;
   const int rsc = c.R * c.S * c.Cs;
+  if (fused_c8(a)) {
+    int ty, tx, nt;
+    c8_tiles(a, ty, tx, nt);
+    hipLaunchKernelGGL(wgrad3x3_c8_kernel, dim3(splits), dim3(NT), 0, s, w, ty, tx, nt);
+    STF_CHECK_LAUNCH();
+    return 0;
+  }
   if (const int pw = fused_pw(a)) {
     int ty, tx, nt;
     fused_tiles(a, pw, ty, tx, nt);

@@ -520,3 +520,31 @@ def test_wgrad_convT2x2_fused(n, cin, cout, h):
     dw = torch.empty(cin * cout * 4, device=DEV)
     nhwc.wgrad(feat_from(x), feat_from(dy), 2, 2, 2, 0, dw)
     assert rel(dw.view_as(w), w.grad) < 2e-3
+
+
+@pytest.mark.parametrize("n,H,W,dycs,dyoff", [
+    (3, 37, 21, 64, 0),         # ragged 16x16 tiles at both edges, fewer tiles than workgroups
+    (16, 64, 64, 64, 0),        # several tiles per workgroup
+    (2, 12, 40, 192, 64),       # dy = slice of a wider concat buffer
+    (8, 256, 256, 64, 0),       # UNet enc1.0 rows (256 x 256), many tiles per workgroup
+])
+def test_wgrad_fused_c8(n, H, W, dycs, dyoff):
+    """Fused-tap weight gradient of the 8-channel-input 3x3 layer (wgrad3x3_c8_kernel: x halo and
+    dy tile in LDS, K split over the waves) vs torch fp32 on the same bf16 operands."""
+    from stfunet import nhwc, _lib
+    import ctypes
+    x = bfr(torch.randn(n, 8, H, W, device=DEV))
+    w = torch.randn(64, 8, 3, 3, device=DEV).requires_grad_(True)
+    y = F.conv2d(x, w, padding=1)
+    dy = bfr(torch.randn_like(y))
+    y.backward(dy)
+    fx, fdy = feat_from(x), feat_from(dy, cs=dycs, off=dyoff)
+    g = _lib.ConvGeom(n, H, W, 8, 8, H, W, 3, 3, 1, 1, 0)
+    a = _lib.WgradArgs(g, fdy.ptr(), fdy.cs, 64, fx.ptr(), None, 0, 0)
+    assert _lib.load().stf_wgrad_kernel_name(ctypes.byref(a)) == b"wgrad3x3_c8_kernel"
+    out = torch.empty(64 * 8 * 9, device=DEV)
+    nhwc.wgrad(fdy, fx, 3, 3, 1, 1, out)
+    assert rel(out.view_as(w), w.grad) < 2e-3
+    out2 = torch.empty_like(out)
+    nhwc.wgrad(fdy, fx, 3, 3, 1, 1, out2)
+    assert torch.equal(out, out2)              # fixed-order fold: repeatable bit for bit
