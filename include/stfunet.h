@@ -353,6 +353,12 @@ int stf_stem_conv7(const float* x, int B, int Ttot, int H, int W, int T, const v
  * zero; grid = stf_stem_conv7_grid(...)), folded with stf_wgrad_reduce(ws, grid, 64, 1, 1, 64, ..). */
 int stf_stem_wgrad7(const float* x, int B, int Ttot, int H, int W, int T, const void* dy, float* ws,
                     stf_stream_t stream);
+/* Input gradient of that stem conv (7x7/s2/p3, Cf input channels; what autograd returns for the
+ * input sequence, src/stf_lstm_unet.py:139-256): dy [T*B][Ho][Wo][64] 16-bit (frame t*B + b), w the
+ * fp32 conv1 weight [64][Cf][7][7] -> dx fp32 in the input's layout [B][Ttot][Cf][H][W], frames
+ * t < T written (t >= T, the PK maps, untouched).  ABI v16. */
+int stf_stem_dgrad7(const void* dy, const float* w, int B, int Ttot, int Cf, int H, int W, int T, float* dx,
+                    stf_stream_t stream);
 /* MaxPool2d(3, 2, 1) of the ResNet stem (src/stf_lstm_unet.py:110,180), NHWC bf16.
  * argmax (uint8 [N][Ho][Wo][C], NULL in eval) records each window's first maximum
  * (index dy*3+dx, torch's tie rule); backward gathers dout over the <= 4 windows

@@ -825,3 +825,77 @@ extern "C" int stf_stem_wgrad7(const float* x, int B, int Ttot, int H, int W, in
   STF_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Input gradient of the stem conv 7x7 / stride 2 / pad 3 (ResNet-34 conv1, src/stf_lstm_unet.py:102;
+// what autograd returns for the input sequence, :139-256): dx[b][t][c][y][x] = sum over the taps
+// (r, s) with y + 3 - r and x + 3 - s even of dy[t*B + b][(y + 3 - r) / 2][(x + 3 - s) / 2][n] *
+// w[n][c][r][s].  A workgroup owns ONE parity class (y & 1, x & 1) of a 32 x 32 input tile, so all
+// of its lanes walk the same 3-4 x 3-4 taps and read the fp32 weights from LDS as broadcasts; each
+// dy row (64 channels, 128 B) is read once per tap and dotted with up to 4 input channels' weights.
+// fp32 accumulation, fp32 weights (the master copy), 16-bit dy as stored.  Not on the training
+// path (train_one_epoch never asks for input gradients).
+constexpr int SD_CC = 4;                                 // input channels per pass (LDS: 4 x 49 x 64 fp32)
+__global__ __launch_bounds__(256) void stem7_dgrad_kernel(const uint16_t* __restrict__ dy, const float* __restrict__ w,
+                                                         int B, int Ttot, int Cf, int H, int W, int Ho, int Wo,
+                                                         int TY, int TX, float* __restrict__ dx) {
+  __shared__ float wl[SD_CC][49][64];
+  const int tid = threadIdx.x;
+  int blk = blockIdx.x;
+  const int cls = blk & 3;
+  blk >>= 2;
+  const int tx = blk % TX, ty = (blk / TX) % TY, img = blk / (TX * TY);
+  const int t = img / B, b = img - t * B;
+  const int cy = cls >> 1, cx = cls & 1;
+  const int y = ty * 32 + 2 * (tid >> 4) + cy, x = tx * 32 + 2 * (tid & 15) + cx;
+  const bool ok = y < H && x < W;
+  const int r0 = (cy + 1) & 1, s0 = (cx + 1) & 1;       // first tap with y + 3 - r even
+  for (int c0 = 0; c0 < Cf; c0 += SD_CC) {
+    const int cc = min(SD_CC, Cf - c0);
+    __syncthreads();
+    for (int i = tid; i < SD_CC * 49 * 64; i += 256) {
+      const int j = i / (49 * 64), k = (i / 64) % 49, n = i % 64;
+      wl[j][k][n] = j < cc ? w[((size_t)n * Cf + c0 + j) * 49 + k] : 0.f;
+    }
+    __syncthreads();
+    float acc[SD_CC] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = r0; r < 7; r += 2) {
+      const int oy = (y + 3 - r) >> 1;
+      for (int s = s0; s < 7; s += 2) {
+        const int ox = (x + 3 - s) >> 1;
+        if (!ok || oy < 0 || oy >= Ho || ox < 0 || ox >= Wo) continue;
+        const uint4* row = reinterpret_cast<const uint4*>(dy + (((size_t)img * Ho + oy) * Wo + ox) * 64);
+        const int k = r * 7 + s;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint4 u = row[q];
+          const uint32_t v[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float lo = e2f(__builtin_bit_cast(e16, (uint16_t)(v[h] & 0xFFFF)));
+            const float hi = e2f(__builtin_bit_cast(e16, (uint16_t)(v[h] >> 16)));
+            const int n = q * 8 + h * 2;
+#pragma unroll
+            for (int j = 0; j < SD_CC; ++j) acc[j] += lo * wl[j][k][n] + hi * wl[j][k][n + 1];
+          }
+        }
+      }
+    }
+    if (ok)
+      for (int j = 0; j < cc; ++j) dx[(((size_t)b * Ttot + t) * Cf + c0 + j) * H * W + (size_t)y * W + x] = acc[j];
+  }
+}
+
+extern "C" int stf_stem_dgrad7(const void* dy, const float* w, int B, int Ttot, int Cf, int H, int W, int T,
+                               float* dx, stf_stream_t stream) {
+  if (!dy || !w || !dx || B < 1 || T < 1 || Ttot < T || Cf < 1 || H < 1 || W < 1) return STF_EINVAL;
+  if ((uintptr_t)dy & 15) return STF_EINVAL;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int TY = (H + 31) / 32, TX = (W + 31) / 32;
+  const long blocks = (long)T * B * TY * TX * 4;
+  if (blocks > 0x7FFFFFFFL) return STF_EINVAL;
+  hipLaunchKernelGGL(stem7_dgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint16_t*)dy, w, B, Ttot, Cf, H, W, Ho, Wo, TY, TX, dx);
+  STF_CHECK_LAUNCH();
+  return 0;
+}

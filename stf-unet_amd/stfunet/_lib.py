@@ -117,6 +117,7 @@ _SIGS = {
     "stf_stem_conv7_grid": (c_int, [c_int, c_int, c_int, c_int]),
     "stf_stem_conv7": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P, P]),
     "stf_stem_wgrad7": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "stf_stem_dgrad7": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "stf_maxpool3s2_fwd": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
     "stf_maxpool3s2_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P, P]),
     "stf_bn_act_maxpool3s2": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),

@@ -336,6 +336,8 @@ class STFProgram:
         self.packs = nhwc.PackCache()
         self.flat = FlatParams(m)
         self.grad_ready_hook = None
+        self.want_dx = False           # set by _STFFunction.backward for an input that requires grad
+        self.dx = None
         self.layers = []
         for layer in (m.layer1, m.layer2, m.layer3, m.layer4):
             progs = []
@@ -717,6 +719,13 @@ class STFProgram:
         dy0 = nhwc.bn_backward_maxpool3(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), S.pool_arg, dout)
         w1 = m.conv1.weight
         kreal = w1[0].numel()
+        if self.want_dx:                       # the input sequence's gradient (no PK maps: P = 0)
+            assert dy0.cs == 64 and dy0.off == 0 and S.P == 0
+            Cf = w1.shape[1]
+            dx = nhwc.empty((B, T, Cf, S.H, S.W), torch.float32, dev)
+            call("stf_stem_dgrad7", dy0.ptr(), _p(w1.detach().float().contiguous()), B, T, Cf, S.H, S.W, T,
+                 _p(dx), stream())
+            self.dx = dx
         if S.xin is None:                      # direct stem conv: the gradient gathers the input too
             assert dy0.cs == 64 and dy0.off == 0
             lib = _lib.load()
@@ -773,11 +782,18 @@ def _check_input_shape(shape, P):
 class _STFFunction(torch.autograd.Function):
     """``res`` = (logits, saved state) of the forward STFLSTMUNet.forward already enqueued: the GPU
     starts on the step while autograd processes the ~160 parameter inputs of this call (~100 us of
-    host time at every synced step boundary)."""
+    host time at every synced step boundary); or None (input gradients: the eager forward runs
+    here)."""
     @staticmethod
     def forward(ctx, x, prog, storage, res, *params):
-        logits, saved = res
-        prog.runtime.own(saved, ctx)
+        ctx.need_dx = ctx.needs_input_grad[0]
+        if res is not None:
+            logits, saved = res
+            prog.runtime.own(saved, ctx)
+        else:
+            need_bwd = any(ctx.needs_input_grad[4:]) or ctx.need_dx
+            with _lib.storage(storage):
+                logits, saved = prog.forward(x, prog.m.training, need_bwd)
         ctx.storage = storage
         ctx.prog, ctx.saved = prog, saved
         return logits.detach()        # the plan's static logits: a fresh tensor object per step
@@ -787,12 +803,17 @@ class _STFFunction(torch.autograd.Function):
         prog = ctx.prog
         dlogits = dlogits.float().contiguous()     # autocast / GradScaler callers: any float dtype
         prog.flat.fresh_grad()
-        with _lib.storage(ctx.storage):
-            prog.runtime.backward(ctx.saved, dlogits)
+        prog.want_dx, prog.dx = ctx.need_dx, None
+        try:
+            with _lib.storage(ctx.storage):
+                prog.runtime.backward(ctx.saved, dlogits)
+        finally:
+            prog.want_dx = False
         ctx.saved = None
         if prog.grad_ready_hook is not None:
             prog.grad_ready_hook(0, ())
-        return (None, None, None, None, *prog.flat.grad_views())
+        dx, prog.dx = prog.dx, None
+        return (dx, None, None, None, *prog.flat.grad_views())
 
 
 class STFLSTMUNet(nn.Module):
@@ -846,12 +867,16 @@ class STFLSTMUNet(nn.Module):
         prog.check_device_errors(x.device)       # step boundary: an earlier step's LSTM timeout raises
         prog.flat.ensure()
         grad = torch.is_grad_enabled()
-        if grad and x.requires_grad:
-            raise NotImplementedError("stfunet.STFLSTMUNet computes parameter gradients only; the input "
-                                      "sequence must not require grad")
-        params = prog.flat.params
-        need_bwd = grad and prog.flat.any_requires_grad()
         storage = _lib.storage_for(self.storage_dtype)
-        with _lib.storage(storage), torch.no_grad():    # (as inside autograd.Function.forward)
-            res = prog.runtime.forward(x, self.training, need_bwd)      # launched before autograd's bookkeeping
-        return {"out": _STFFunction.apply(x, prog, storage, res, *params)}
+        res = None
+        if grad and x.requires_grad:
+            # the input gradient (reference autograd returns it, src/stf_lstm_unet.py:139-256): the
+            # eager forward inside the autograd Function, the stem's input gradient in the backward
+            if self.use_pk_maps:
+                raise NotImplementedError("stfunet.STFLSTMUNet: input gradients with PK-map inputs (the PK "
+                                          "maps' resize / fusion path) are not implemented")
+        else:
+            need_bwd = grad and prog.flat.any_requires_grad()
+            with _lib.storage(storage), torch.no_grad():    # (as inside autograd.Function.forward)
+                res = prog.runtime.forward(x, self.training, need_bwd)      # launched before autograd's bookkeeping
+        return {"out": _STFFunction.apply(x, prog, storage, res, *prog.flat.params)}

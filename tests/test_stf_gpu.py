@@ -501,12 +501,67 @@ def test_stf_eval_mode_backward_vs_oracle():
     assert not bad, bad
 
 
-def test_stf_input_gradient_rejected():
+def test_stf_input_gradient_vs_oracle():
+    """x.requires_grad: the input sequence's gradient (reference autograd returns it,
+    src/stf_lstm_unet.py:139-256) -- the eager forward, then the stem's stf_stem_dgrad7 after the
+    backward -- vs autograd of the fp32 oracle in eval mode (within 2x the bf16 emulation's error +
+    0.02, as the parameter gradients above); the parameter gradients are those of the plain call."""
+    import oracle.unet_bf16 as o_q
+    from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
+    from oracle.init import canonical_state_dict
     from stfunet import STFLSTMUNet
-    m = STFLSTMUNet(time_steps=2).to(DEV)
-    x = torch.randn(1, 2, 1, 64, 64, device=DEV, requires_grad=True)
+    from stfunet.loss import criterion
+    g = np.load(os.path.join(GOLDEN, "stf_t4.npz"))
+    m = STFLSTMUNet(time_steps=4)
+    sd = canonical_state_dict(m.state_dict(), seed=0)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["target"])
+    p = {k: v.clone() for k, v in sd.items()}
+    xo = x.clone().requires_grad_(True)
+    o_loss.criterion(o_stf.forward(p, xo, False)["out"], t).backward()
+    xe = x.clone().requires_grad_(True)
+    with o_q.storage(torch.bfloat16):
+        o_loss.criterion(o_emu.forward(p, xe, False)["out"], t).backward()
+    xh = x.to(DEV).requires_grad_(True)
+    criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
+    assert xh.grad is not None and xh.grad.shape == x.shape and torch.isfinite(xh.grad).all()
+    e_hip, e_emu = rel(xh.grad, xo.grad), rel(xe.grad, xo.grad)
+    assert e_hip < 2 * e_emu + 0.02, (e_hip, e_emu)
+    grads = {k: v.grad.clone() for k, v in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    criterion({"out": m(x.to(DEV))["out"]}, t.to(DEV)).backward()      # the planned path, no input grad
+    for k, v in m.named_parameters():
+        assert torch.equal(v.grad, grads[k]), k
+
+
+def test_stf_input_gradient_pk_rejected():
+    from stfunet import STFLSTMUNet
+    m = STFLSTMUNet(time_steps=2, use_pk_maps=True).to(DEV)
+    x = torch.randn(1, 5, 1, 64, 64, device=DEV, requires_grad=True)
     with pytest.raises(NotImplementedError):
         m(x)
+
+
+@pytest.mark.parametrize("B,T,Cf,H,W", [(2, 3, 1, 45, 38), (1, 2, 3, 64, 33), (1, 1, 6, 32, 32)])
+def test_stem_dgrad7_vs_torch(B, T, Cf, H, W):
+    """stf_stem_dgrad7 (the stem conv's input gradient, parity-class workgroups, fp32 weights)
+    vs torch's conv2d input gradient in fp32 on the same 16-bit dy (odd sizes: ragged tiles and
+    partial tap sets at the borders; 6 channels: two channel passes)."""
+    from stfunet import _lib
+    from stfunet._lib import call, stream
+    from stfunet.nhwc import _p
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    w = torch.randn(64, Cf, 7, 7, device=DEV) / (Cf * 49) ** 0.5
+    dy = torch.randn(T * B, 64, Ho, Wo, device=DEV).to(_lib.storage_dtype())
+    dyf = dy.float()
+    ref = torch.nn.grad.conv2d_input((T * B, Cf, H, W), w, dyf, stride=2, padding=3)     # [t*B + b]
+    ref = ref.view(T, B, Cf, H, W).transpose(0, 1)
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    dx = torch.full((B, T, Cf, H, W), float("nan"), device=DEV)
+    call("stf_stem_dgrad7", _p(dyn), _p(w), B, T, Cf, H, W, T, _p(dx), stream())
+    torch.cuda.synchronize()
+    assert rel(dx, ref) < 1e-5
 
 
 def test_stem_bn_act_maxpool_fused_equals_two_passes():
