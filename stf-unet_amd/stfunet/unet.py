@@ -101,7 +101,15 @@ class DoubleConvProgram:
         if not need_dsrc:
             return None
         dsrc = new_feat(s.src.N, s.src.H, s.src.W, s.src.C, s.src.buf.device)
-        nhwc.conv_dgrad(dy1, conv1.weight, dsrc, 3, 3, 1, 1)
+        w1 = conv1.weight
+        if s.src.C != w1.shape[1]:
+            # zero-padded input channels (in_channels % 8 != 0): the weight padded the same way, so the
+            # padded channels' gradient is computed and dropped by the caller
+            cin = w1.shape[1]
+            wp = nhwc.memset0(nhwc.empty((self.cout, s.src.C, 3, 3), torch.float32, w1.device))
+            nhwc.copy_rows(w1.detach(), cin * 9, wp, s.src.C * 9, self.cout, cin * 9)
+            w1 = wp
+        nhwc.conv_dgrad(dy1, w1, dsrc, 3, 3, 1, 1)
         return dsrc
 
     def _wgrad_conv1(self, dy1, src, out):
@@ -279,9 +287,6 @@ class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, prog, storage, res, *params):
         ctx.need_dx = ctx.needs_input_grad[0]
-        if ctx.need_dx and prog.m.in_channels % 8:
-            raise NotImplementedError("input gradients need in_channels % 8 == 0 (the input is not "
-                                      "channel-padded then)")
         if res is not None:
             logits, saved = res
             prog.runtime.own(saved, ctx)

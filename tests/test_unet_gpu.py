@@ -41,9 +41,9 @@ def _bn_fed_bias(k):
     return k.endswith((".0.bias", ".3.bias")) and not k.startswith(("up", "out_conv"))
 
 
-def _model(base_c, seed=0):
+def _model(base_c, seed=0, in_channels=8):
     from stfunet.unet import UNet
-    m = UNet(in_channels=8, num_classes=2, base_c=base_c)
+    m = UNet(in_channels=in_channels, num_classes=2, base_c=base_c)
     sd = canonical_state_dict(m.state_dict(), seed=seed)
     m.load_state_dict(sd)
     return m.to(DEV), sd
@@ -323,15 +323,16 @@ def test_unet_eval_mode_backward_vs_oracle():
             assert torch.count_nonzero(prm.grad) == 0, k
 
 
-@pytest.mark.parametrize("train", [True, False])
-def test_unet_input_gradient_vs_oracle(train):
+@pytest.mark.parametrize("train,cin", [(True, 8), (False, 8), (True, 1), (False, 3)])
+def test_unet_input_gradient_vs_oracle(train, cin):
     """d(loss)/d(input) (autograd of the input tensor, e.g. saliency maps) vs the fp32
     oracle, within 2x the bf16-storage emulation's error + 0.03; the parameter gradients
-    of the same backward are unchanged by asking for it."""
+    of the same backward are unchanged by asking for it.  cin 1 / 3: the input is zero-padded
+    to 8 channels, the padded channels' gradient dropped (configs[0] is a 1-channel UNet)."""
     from stfunet.loss import criterion
-    model, sd = _model(8, seed=6)
+    model, sd = _model(8, seed=6, in_channels=cin)
     x5, t = dce_case(7, 2, 8, 64, 64)
-    x = x5.flatten(1, 2)
+    x = x5.flatten(1, 2)[:, :cin].contiguous()
     res = []
     for fwd in (o_unet.forward, o_unet_bf16.forward):
         p = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
