@@ -118,8 +118,15 @@ def pmc_mfma(kernel, workload):
         if d.get("workload") != workload:
             continue
         k = d.get("kernels", {}).get(kernel)
-        return ({"mfma_busy_util": k["mfma_busy_util"], "clock_ghz": k["clock_ghz"], "source": os.path.relpath(path, HERE)}
-                if k else None)
+        if not k:
+            return None
+        src = os.path.relpath(path, HERE)
+        if k.get("clock_reliable") is False and "mfma_busy_util_step_clock" in k:
+            # dispatches under ~0.3 ms read their own GRBM clock high (above the chip's 2.4 GHz):
+            # the busy fraction at the step clock (slope of cycles against duration over the step)
+            return {"mfma_busy_util": k["mfma_busy_util_step_clock"], "clock_ghz": d.get("step_clock_ghz"),
+                    "clock_from": "step clock: " + str(d.get("step_clock_from", "")), "source": src}
+        return {"mfma_busy_util": k["mfma_busy_util"], "clock_ghz": k["clock_ghz"], "source": src}
     return None
 
 
