@@ -529,6 +529,7 @@ class STFProgram:
         # ---- encoder; layer outputs land in the LSTM [x | h] buffers (or PK concat);
         # lstm li (li < 3) starts on its side stream as soon as layer li is done
         S.enc, S.lbuf, S.pkbuf = [], [], []
+        S.dpk_parts = []                 # the input gradient's PK-map shares (eager input-gradient backward)
         side = self.side_streams(dev)
         main = torch.cuda.current_stream(dev)
         S.lstm = [None] * 4
@@ -719,13 +720,8 @@ class STFProgram:
         dy0 = nhwc.bn_backward_maxpool3(S.y0, S.bn0, m.bn1, gv(m.bn1.weight), gv(m.bn1.bias), S.pool_arg, dout)
         w1 = m.conv1.weight
         kreal = w1[0].numel()
-        if self.want_dx:                       # the input sequence's gradient (no PK maps: P = 0)
-            assert dy0.cs == 64 and dy0.off == 0 and S.P == 0
-            Cf = w1.shape[1]
-            dx = nhwc.empty((B, T, Cf, S.H, S.W), torch.float32, dev)
-            call("stf_stem_dgrad7", dy0.ptr(), _p(w1.detach().float().contiguous()), B, T, Cf, S.H, S.W, T,
-                 _p(dx), stream())
-            self.dx = dx
+        if self.want_dx:
+            self.dx = self._input_grad(S, dy0, w1, B, T, P, dev)
         if S.xin is None:                      # direct stem conv: the gradient gathers the input too
             assert dy0.cs == 64 and dy0.off == 0
             lib = _lib.load()
@@ -746,6 +742,34 @@ class STFProgram:
             nhwc.wgrad(dy0, S.xin, 1, 1, 1, 0, tmp, defer=False)
             nhwc.copy_rows(tmp, S.xin.C, gv(w1), kreal, w1.shape[0], kreal)
 
+    def _input_grad(self, S, dy0, w1, B, T, P, dev):
+        """d(loss)/d(x) for x [B, T + P, Cf, H, W]: the stem conv's input gradient over its Cf + P input
+        channels (frame t's channels, then the P PK maps every frame's stem also reads,
+        src/stf_lstm_unet.py:146-160), plus with PK maps the fusion branches' gradient w.r.t. the
+        resized maps (saved by _pk_fusion_backward) taken back through the bilinear resize
+        (align_corners=True, stf_bilinear_ac_bwd), summed over the T frames and the 4 scales."""
+        assert dy0.cs == 64 and dy0.off == 0
+        H, W = S.H, S.W
+        cin = w1.shape[1]
+        Cf = cin - P
+        dxt = nhwc.empty((B, T, cin, H, W), torch.float32, dev)
+        call("stf_stem_dgrad7", dy0.ptr(), _p(w1.detach().float().contiguous()), B, T, cin, H, W, T, _p(dxt),
+             stream())
+        if P == 0:
+            return dxt
+        dx = nhwc.empty((B, T + P, Cf, H, W), torch.float32, dev)
+        dx[:, :T].copy_(dxt[:, :, :Cf])
+        dpk = dxt[:, :, Cf:].sum(1)                                     # [B, P, H, W]
+        for part in S.dpk_parts:                                        # [T*B, h, w, C + 8]: [.., C:C+P]
+            C = part.C - 8
+            src = part.slice(C, 8)
+            g = new_feat(T * B, H, W, 8, dev)
+            call("stf_bilinear_ac_bwd", src.ptr(), T * B, part.H, part.W, 8, src.cs, g.ptr(), H, W, 8, stream())
+            dpk += g.buf.view(T, B, H, W, 8)[..., :P].float().sum(0).permute(0, 3, 1, 2)
+        S.dpk_parts = []
+        dx[:, T:, 0].copy_(dpk)                                         # (PK maps: Cf == 1)
+        return dx
+
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
         fus = getattr(self.m, f"pk_fusion{k + 1}")
         pkb = S.pkbuf[k]
@@ -759,6 +783,8 @@ class STFProgram:
         w = nhwc.memset0(nhwc.empty((C, pkb.C, 1, 1), torch.float32, de.buf.device))
         nhwc.copy_rows(fus.weight.detach(), cin, w, pkb.C, C, cin)
         nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0)
+        if self.want_dx:                  # the resized PK maps' share, for _input_grad
+            S.dpk_parts.append(dpk)
         return dpk.slice(0, C)
 
 
@@ -872,9 +898,8 @@ class STFLSTMUNet(nn.Module):
         if grad and x.requires_grad:
             # the input gradient (reference autograd returns it, src/stf_lstm_unet.py:139-256): the
             # eager forward inside the autograd Function, the stem's input gradient in the backward
-            if self.use_pk_maps:
-                raise NotImplementedError("stfunet.STFLSTMUNet: input gradients with PK-map inputs (the PK "
-                                          "maps' resize / fusion path) are not implemented")
+            # (with PK maps also their fusion branches' gradient through the resize)
+            pass
         else:
             need_bwd = grad and prog.flat.any_requires_grad()
             with _lib.storage(storage), torch.no_grad():    # (as inside autograd.Function.forward)

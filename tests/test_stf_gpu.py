@@ -535,12 +535,34 @@ def test_stf_input_gradient_vs_oracle():
         assert torch.equal(v.grad, grads[k]), k
 
 
-def test_stf_input_gradient_pk_rejected():
+def test_stf_input_gradient_pk_vs_oracle():
+    """The same with PK maps on the T axis (x [B, T + 3, 1, H, W]): the frames' gradient from the
+    stem, the PK maps' from the stem (every frame reads them) plus the four fusion branches through
+    the bilinear resize's backward, summed over the frames -- vs autograd of the fp32 oracle."""
+    import oracle.unet_bf16 as o_q
+    from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
+    from oracle.init import canonical_state_dict
     from stfunet import STFLSTMUNet
-    m = STFLSTMUNet(time_steps=2, use_pk_maps=True).to(DEV)
-    x = torch.randn(1, 5, 1, 64, 64, device=DEV, requires_grad=True)
-    with pytest.raises(NotImplementedError):
-        m(x)
+    from stfunet.loss import criterion
+    m = STFLSTMUNet(time_steps=3, use_pk_maps=True)
+    sd = canonical_state_dict(m.state_dict(), seed=1)
+    m.load_state_dict(sd)
+    m = m.to(DEV).eval()
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(2, 6, 1, 96, 64, generator=gen)
+    t = torch.randint(0, 2, (2, 48, 32), generator=gen)
+    p = {k: v.clone() for k, v in sd.items()}
+    xo = x.clone().requires_grad_(True)
+    o_loss.criterion(o_stf.forward(p, xo, False, use_pk_maps=True)["out"], t).backward()
+    xe = x.clone().requires_grad_(True)
+    with o_q.storage(torch.bfloat16):
+        o_loss.criterion(o_emu.forward(p, xe, False, use_pk_maps=True)["out"], t).backward()
+    xh = x.to(DEV).requires_grad_(True)
+    criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
+    assert xh.grad is not None and xh.grad.shape == x.shape and torch.isfinite(xh.grad).all()
+    for sl in (slice(0, 3), slice(3, 6)):                  # frames, PK maps
+        e_hip, e_emu = rel(xh.grad[:, sl], xo.grad[:, sl]), rel(xe.grad[:, sl], xo.grad[:, sl])
+        assert e_hip < 2 * e_emu + 0.02, (sl, e_hip, e_emu)
 
 
 @pytest.mark.parametrize("B,T,Cf,H,W", [(2, 3, 1, 45, 38), (1, 2, 3, 64, 33), (1, 1, 6, 32, 32)])
