@@ -1655,7 +1655,7 @@ __global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_halo4_kernel(Geo
 // kernel's DIRECT epilogue, so each lane stores 16-B chunks of 8 consecutive channels straight
 // from its accumulators; BN partial sums per (statistics group, workgroup) from the stored values.
 constexpr int C8_T = 16, C8_HW = C8_T + 2, C8_HR = C8_HW * C8_HW;      // 324 halo rows per tile
-__global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int TX, int per, int rem) {
+__global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int TX, int per, int rem, int c8_full) {
   __shared__ __attribute__((aligned(16))) uint4 halo[2][C8_HR];
   __shared__ float red[4][2][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1773,13 +1773,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int T
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(wf[j][ks], xf[i], acc[i][j]);
     }
-    // epilogue: pixel (row wave * 4 + i, column fr) of the tile; two 16-B stores per pixel
+    // epilogue: lane (fr, fk) holds chunks fk (h = 0) and 4 + fk (h = 1) of pixel (row wave * 4 + i,
+    // column fr).  C8_FULL (default): the h = 1 chunk goes to lane fr ^ 8 (DPP row_ror:8) so that each
+    // store instruction writes 8 whole 128-B pixel rows (pixels 0-7, then 8-15: lanes fr < 8 own
+    // chunk fk, lanes fr >= 8 the partner's chunk 4 + fk) instead of half of 16 rows
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int y = ty * C8_T + wave * 4 + i, x = tx * C8_T + fr;
       const bool ok = y < a.Hd && x < a.Wd;
       const size_t m = ((size_t)img * a.Hd + y) * a.Wd + x;
+      uint4 u[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         float f[8];
@@ -1788,12 +1792,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c8_kernel(Geo a, int TY, int T
           f[r] = round_e(acc[i][2 * h][r] + bv[h][r]);
           f[4 + r] = round_e(acc[i][2 * h + 1][r] + bv[h][4 + r]);
         }
-        const uint4 u = pack8(f);
-        const uint32_t off = ok ? (uint32_t)((m * a.dcs + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        u[h] = pack8(f);
         if (ok) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) { s1[h][e] += f[e]; s2[h][e] += f[e] * f[e]; }
+        }
+      }
+      if (c8_full) {
+        const uint4 rcv = make_uint4(__builtin_amdgcn_update_dpp(0u, u[1].x, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u[1].y, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u[1].z, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u[1].w, 0x128, 0xF, 0xF, false));
+        const bool lo = fr < 8;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          // half 0: pixels 0-7 of the tile row, half 1: pixels 8-15
+          const uint4 v = (half == 0) == lo ? u[0] : rcv;
+          const int px = (fr & 7) + half * 8, ch = ((half == 0) == lo ? 0 : 32) + fk * 8;
+          const int xx = tx * C8_T + px;
+          const size_t mm = ((size_t)img * a.Hd + y) * a.Wd + xx;
+          const uint32_t off = (y < a.Hd && xx < a.Wd) ? (uint32_t)((mm * a.dcs + ch) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rs_dst, off, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t off = ok ? (uint32_t)((m * a.dcs + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{u[h].x, u[h].y, u[h].z, u[h].w}, rs_dst, off, 0, 0);
         }
       }
     }
@@ -2244,7 +2269,10 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     if ((g.Mg % (c.Hd * c.Wd)) != 0) return STF_EINVAL;
     const int TY = (c.Hd + C8_T - 1) / C8_T, TX = (c.Wd + C8_T - 1) / C8_T;
     const int tiles = c8_tiles(c), grid = c8_grid(a);
-    hipLaunchKernelGGL(conv3x3_c8_kernel, dim3(grid), dim3(256), 0, s, g, TY, TX, tiles / grid, tiles % grid);
+    // whole-pixel-row stores (STF_C8_FULL=0: the half-row stores, A/B)
+    static const int c8_full = stf::ab_switch("STF_C8_FULL", 1) != 0;
+    hipLaunchKernelGGL(conv3x3_c8_kernel, dim3(grid), dim3(256), 0, s, g, TY, TX, tiles / grid, tiles % grid,
+                       c8_full);
     STF_CHECK_LAUNCH();
     return 0;
   }
