@@ -43,6 +43,8 @@ struct Geo {
   // halo kernel: keep a ring stage's weight rows across items when they are the rows
   // the next fill needs (same 64-channel output slice and source chunk)
   int wkeep;
+  // halo direct epilogue: whole 128-B pixel rows per store instruction (lane exchange fr <-> fr ^ 8)
+  int full;
 };
 
 STF_DEV int swz(int row, int kc) { return kc ^ ((-(row >> 2)) & 3); }
@@ -1246,15 +1248,41 @@ __device__ __forceinline__ void halo_body(Geo a, uint32_t src_bytes, int TY, int
         }
       }
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
+    if (!BNR && IX == 1 && a.full) {
+      // (not with the fused BN-backward reduction, nor in the multi-image kernels: their registers
+      // leave no room -- they spilled)
+      // lane (fr, fk) holds chunks fk (h = 0) and 4 + fk (h = 1) of pixel i*16 + fr: its h = 1 chunk
+      // and pixel index go to lane fr ^ 8 (DPP row_ror:8), so each store writes 8 whole 128-B pixel
+      // rows (pixels 0-7 of the group, then 8-15) instead of half of 16 -- as many stores
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const uint4 u = uq[h][i];
-        const uint32_t off =
-            mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        const uint4 u1 = uq[1][i];
+        const uint4 rcv = make_uint4(__builtin_amdgcn_update_dpp(0u, u1.x, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u1.y, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u1.z, 0x128, 0xF, 0xF, false),
+                                     __builtin_amdgcn_update_dpp(0u, u1.w, 0x128, 0xF, 0xF, false));
+        const int mx = __builtin_amdgcn_update_dpp(0, mq[i], 0x128, 0xF, 0xF, false);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const bool own = (half == 0) == (fr < 8);
+          const uint4 v = own ? uq[0][i] : rcv;
+          const int m = own ? mq[i] : mx;
+          const int ch = (own ? 0 : 32) + fk * 8;
+          const uint32_t off = m >= 0 ? (uint32_t)(((size_t)m * a.dcs + nt * BN + ch) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rs_dst, off, 0, 0);
+        }
       }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const uint4 u = uq[h][i];
+          const uint32_t off =
+              mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + fk * 8) * 2) : 0xFFFFFFF0u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+        }
+    }
     float res[2] = {0.f, 0.f};                           // row16_reduce_scatter results per half
     if constexpr (BNR) {
       // g = dz * [y*scale+shift > 0]; (sum g, sum g*xhat), like stf_bn_bwd_reduce
@@ -2239,6 +2267,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
   g.ksplit = 1; g.ws = nullptr;
   static const int wkeep = stf::ab_switch("STF_HALO_WKEEP", 1);
   g.wkeep = wkeep;
+  static const int full = stf::ab_switch("STF_HALO_FULL", 1);
+  g.full = full;
   if (a->bnr) {
     g.bnr_y = (const uint16_t*)a->bnr->y; g.bnr_ycs = a->bnr->y_cstride;
     g.bnr_scale = a->bnr->scale; g.bnr_shift = a->bnr->shift; g.bnr_mean = a->bnr->mean;
