@@ -541,7 +541,7 @@ def test_wgrad_fused_c8(n, H, W, dycs, dyoff):
     fx, fdy = feat_from(x), feat_from(dy, cs=dycs, off=dyoff)
     g = _lib.ConvGeom(n, H, W, 8, 8, H, W, 3, 3, 1, 1, 0)
     a = _lib.WgradArgs(g, fdy.ptr(), fdy.cs, 64, fx.ptr(), None, 0, 0)
-    assert _lib.load().stf_wgrad_kernel_name(ctypes.byref(a)) == b"wgrad3x3_c8_kernel"
+    assert _lib.load().stf_wgrad_kernel_name(ctypes.byref(a)).startswith(b"wgrad3x3_c8_kernel")
     out = torch.empty(64 * 8 * 9, device=DEV)
     nhwc.wgrad(fdy, fx, 3, 3, 1, 1, out)
     assert rel(out.view_as(w), w.grad) < 2e-3
