@@ -361,7 +361,7 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
 
     from stfunet import engine, nhwc, plan
-    from stfunet.ddp import GradAllReduce
+    from stfunet.ddp import GradAllReduce, rccl_stream_note
     from stfunet.flops import stf_train_flops, unet_train_flops
     from stfunet.optim import AdamW
     from stfunet.synthetic import dce_batch
@@ -500,6 +500,7 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": args.time_steps, "image": [args.size, args.size],
                        "parallelism": f"dp{world}", "ddp_hook": bool(ddp is not None)},
+            **({"rccl_stream": rccl_stream_note()} if ddp is not None else {}),
             "train_gflop_per_sample": round(train_gflop, 2),
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
             "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
@@ -515,6 +516,22 @@ def main():
         if not args.no_cpu_baseline and world == 1:      # reported baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)
+    # Explicit teardown, in dependency order, while the HIP runtime and the process group are
+    # still up: the hook, the recorded step plans (their events, kernels' argument blocks and
+    # private memory pools), the model's buffers, then the process group -- nothing of ours is
+    # left for interpreter shutdown / __cxa_finalize to destroy after the runtime's own teardown
+    # (a --hook run under rocprofv3 took SIGSEGV inside __cxa_finalize in round 5)
+    torch.cuda.synchronize()
+    prog = getattr(model, "_program", None)
+    if prog is not None:
+        prog.grad_ready_hook = None
+        prog.runtime.close()
+    del ddp, prog, runtime, model, opt, sched, batches, loss
+    plan.drain_pools()
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()

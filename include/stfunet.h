@@ -446,6 +446,12 @@ int stf_bilinear_ac_fwd(const void* x, int N, int H, int W, int C, int x_cstride
                         int y_cstride, stf_stream_t stream);
 int stf_bilinear_ac_bwd(const void* dy, int N, int h, int w, int C, int dy_cstride, void* dx, int H, int W,
                         int dx_cstride, stf_stream_t stream);
+/* The PK maps' share of the input gradient (ABI v17): dy = T frames of B images [T*B][h][w] (t-major,
+ * channels [0, 8) of stride dy_cstride, 16-bit NHWC), summed over the frames in fp32 at (h, w) and taken
+ * back through the same resize; channels [0, P) (P <= 8) are ADDED to the fp32 out[b*out_bstride +
+ * c*out_cstride + y*W + x] (x [B][T+P][1][H][W]: out = &x[0][T], strides (T+P)*H*W and H*W). */
+int stf_bilinear_ac_bwd_tsum(const void* dy, int T, int B, int h, int w, int dy_cstride, int P, float* out,
+                             int64_t out_bstride, int64_t out_cstride, int H, int W, stf_stream_t stream);
 /* dwcat [4C][2C] / dbias [4C] (interleaved) -> torch-layout dW_ih, dW_hh, db_ih, db_hh. */
 int stf_lstm_unpack_grad(const float* dwcat, const float* dbias, int C, float* dw_ih,
                          float* dw_hh, float* db_ih, float* db_hh, stf_stream_t stream);

@@ -395,7 +395,7 @@ extern "C" const char* stf_error_string(int code) {
   return hipGetErrorString((hipError_t)code);
 }
 
-extern "C" int stf_abi_version(void) { return 16; }
+extern "C" int stf_abi_version(void) { return 17; }
 
 extern "C" int stf_storage_type(void) {
 #ifdef STF_FP16

@@ -404,6 +404,54 @@ __global__ void bilinear_ac_bwd_kernel(const uint16_t* __restrict__ dy, int N, i
   }
 }
 
+// The same gather for the PK maps' input gradient (ABI v17): dy holds T frames of B images
+// (t-major, [T*B][h][w], channels [0, 8) of stride dycs); the T frames are summed in fp32 at the
+// low resolution (the resize is linear and the same for every frame) and the first P channels of
+// the full-resolution sum are ADDED to out[b*obs + c*ocs + y*W + x] (fp32, the input's layout)
+__global__ void bilinear_ac_bwd_tsum_kernel(const uint16_t* __restrict__ dy, int T, int B, int h, int w,
+                                            int dycs, int P, float* __restrict__ out, long obs, long ocs, int H,
+                                            int W) {
+  const long units = (long)B * H * W;
+  const float sy = h > 1 ? (float)(H - 1) / (float)(h - 1) : 0.f;
+  const float sx = w > 1 ? (float)(W - 1) / (float)(w - 1) : 0.f;
+  for (long p = blockIdx.x * (long)NT + threadIdx.x; p < units; p += (long)gridDim.x * NT) {
+    const int ix = (int)(p % W);
+    const long r = p / W;
+    const int iy = (int)(r % H), b = (int)(r / H);
+    const int oy0 = sy > 0.f ? max(0, (int)((float)(iy - 1) / sy) - 1) : 0;
+    const int oy1 = sy > 0.f ? min(h - 1, (int)((float)(iy + 1) / sy) + 1) : h - 1;
+    const int ox0 = sx > 0.f ? max(0, (int)((float)(ix - 1) / sx) - 1) : 0;
+    const int ox1 = sx > 0.f ? min(w - 1, (int)((float)(ix + 1) / sx) + 1) : w - 1;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      int y0, y1;
+      float ly;
+      ac_coord(oy, sy, H, y0, y1, ly);
+      const float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        int x0, x1;
+        float lx;
+        ac_coord(ox, sx, W, x0, x1, lx);
+        const float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int t = 0; t < T; ++t) {
+          float g[8];
+          unpack8(*reinterpret_cast<const uint4*>(dy + ((((long)t * B + b) * h + oy) * w + ox) * dycs), g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += g[j];
+        }
+        const float k = wy * wx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += k * s[j];
+      }
+    }
+    float* o = out + (long)b * obs + (long)iy * W + ix;
+    for (int c = 0; c < P; ++c) o[c * ocs] += acc[c];
+  }
+}
+
 
 // Direct 7x7 / stride 2 / pad 3 stem convolution of a 1-channel frame sequence (ResNet-34 conv1,
 // src/stf_lstm_unet.py:108,177) into NHWC bf16 [T*B][Ho][Wo][64], with the grouped BatchNorm
@@ -685,6 +733,19 @@ extern "C" int stf_bilinear_ac_bwd(const void* dy, int N, int h, int w, int C, i
   const long units = (long)N * H * W * (C / 8);
   hipLaunchKernelGGL(bilinear_ac_bwd_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
                      (const uint16_t*)dy, N, h, w, C, dy_cstride, (uint16_t*)dx, H, W, dx_cstride);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int stf_bilinear_ac_bwd_tsum(const void* dy, int T, int B, int h, int w, int dy_cstride, int P,
+                                        float* out, int64_t out_bstride, int64_t out_cstride, int H, int W,
+                                        stf_stream_t stream) {
+  if (!dy || !out || T < 1 || B < 1 || H < 1 || W < 1 || h < 1 || w < 1 || P < 1 || P > 8 || dy_cstride < 8 ||
+      dy_cstride % 8 || ((uintptr_t)dy & 15) || out_bstride < 1 || out_cstride < 1)
+    return STF_EINVAL;
+  const long units = (long)B * H * W;
+  hipLaunchKernelGGL(bilinear_ac_bwd_tsum_kernel, dim3(grid_for(units, 8192)), dim3(NT), 0, (hipStream_t)stream,
+                     (const uint16_t*)dy, T, B, h, w, dy_cstride, P, out, (long)out_bstride, (long)out_cstride, H, W);
   STF_CHECK_LAUNCH();
   return 0;
 }

@@ -12,7 +12,11 @@ reduces the last bucket and makes the compute stream wait.
 
 Gradients written on side streams (the STF program's LSTM backwards and weight-gradient
 stream) reach the hook as ``deps``.  A bucket's collective is enqueued ON the joiner stream
-(``async_op=False`` under it: RCCL launches on the current stream, the host does not block),
+(``async_op=False`` under it: with PyTorch >= 2.7 -- 2.10 here -- ProcessGroupNCCL launches a
+synchronous collective on the CURRENT stream and the host does not block; an older build that
+still launches on the process group's internal stream stays correct, because a synchronous call
+makes the current stream (the joiner) wait for that stream, but then the hardware-queue argument
+below and its measured 3-5 % no longer hold -- ``rccl_stream_note()`` says which applies),
 after the joiner waits for the compute stream and those side streams -- so the compute stream
 never waits for a side stream on the hook's account, and no stream of RCCL's own is involved:
 on HIP, streams share GPU_MAX_HW_QUEUES hardware queues (4) and two streams on one queue run in
@@ -27,6 +31,14 @@ amortise both.
 """
 import torch
 import torch.distributed as dist
+
+
+def rccl_stream_note():
+    """Which stream a synchronous RCCL collective runs on under this PyTorch build (the
+    assumption the joiner design rests on), for bench output."""
+    v = tuple(int(p) for p in torch.__version__.split("+")[0].split(".")[:2])
+    return ("current stream (the joiner)" if v >= (2, 7) else
+            "process group's internal stream (joined by the current stream)") + f", torch {torch.__version__}"
 
 
 class GradAllReduce:

@@ -305,16 +305,18 @@ def _pack_into(w, mode, cpad, out, launch=True):
     return out
 
 
-def pack_weight(w, mode, cpad=0):
+def pack_weight(w, mode, cpad=0, cache=True):
     """fp32 master weight -> 16-bit GEMM rows (modes: include/stfunet.h); served
-    from the active program's PackCache when one is running."""
-    if ACTIVE_PACKS is not None:
+    from the active program's PackCache when one is running.  ``cache=False`` for
+    per-call temporaries (a zero-padded copy of a weight): the PackCache keys by
+    address and would keep every dead temporary alive."""
+    if cache and ACTIVE_PACKS is not None:
         return ACTIVE_PACKS.get(w, mode, cpad)
     w = w.detach()
     assert w.dtype == torch.float32 and w.is_contiguous()
     d0, d1, R, S = w.shape
     n = d0 * R * S * cpad if mode == 0 else d0 * d1 * R * S
-    out = torch.empty(n, dtype=sdt(), device=w.device)
+    out = empty(n, sdt(), w.device)
     call("stf_pack_weight", _p(w), d0, d1, R, S, mode, cpad, _p(out), stream())
     return out
 
@@ -420,17 +422,19 @@ def _plan_tag(a, fn, key, flops):
     call("stf_plan_tag", _kernel_name(fn, key, a).encode(), float(flops))
 
 
-def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None):
+def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None, cache=True):
     """Conv2d input gradient: stride 1 runs as a forward gather over flipped taps
     (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather.
     ``accumulate``: dx += gradient (residual / multi-consumer tensors).
     ``bnr`` = (y, BNState, relu): dx feeds the backward of act(BN(y)); returns the
-    fused partial sums and tiles for bn_backward_fused."""
+    fused partial sums and tiles for bn_backward_fused.  ``cache=False``: ``w`` is a per-call
+    temporary (pack_weight)."""
     groups = bnr[1].groups if bnr is not None else 1
     if stride == 1 and 2 * pad == R - 1 and R == S:
-        return igemm(dy, pack_weight(w, 5), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate, bnr=bnr,
-                     groups=groups)
-    return igemm(dy, pack_weight(w, 1), dx.C, dx, R, S, stride, pad, transposed=True, accumulate=accumulate,
+        return igemm(dy, pack_weight(w, 5, cache=cache), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate,
+                     bnr=bnr, groups=groups)
+    return igemm(dy, pack_weight(w, 1, cache=cache), dx.C, dx, R, S, stride, pad, transposed=True,
+                 accumulate=accumulate,
                  bnr=bnr, groups=groups)
 
 

@@ -759,15 +759,14 @@ class STFProgram:
             return dxt
         dx = nhwc.empty((B, T + P, Cf, H, W), torch.float32, dev)
         dx[:, :T].copy_(dxt[:, :, :Cf])
-        dpk = dxt[:, :, Cf:].sum(1)                                     # [B, P, H, W]
+        dx[:, T:, 0].copy_(dxt[:, :, Cf:].sum(1))                       # (PK maps: Cf == 1)
         for part in S.dpk_parts:                                        # [T*B, h, w, C + 8]: [.., C:C+P]
             C = part.C - 8
             src = part.slice(C, 8)
-            g = new_feat(T * B, H, W, 8, dev)
-            call("stf_bilinear_ac_bwd", src.ptr(), T * B, part.H, part.W, 8, src.cs, g.ptr(), H, W, 8, stream())
-            dpk += g.buf.view(T, B, H, W, 8)[..., :P].float().sum(0).permute(0, 3, 1, 2)
+            # summed over the T frames at the low resolution in fp32, resized once, added into dx
+            call("stf_bilinear_ac_bwd_tsum", src.ptr(), T, B, part.H, part.W, src.cs, P, _p(dx[:, T:]),
+                 (T + P) * H * W, H * W, H, W, stream())
         S.dpk_parts = []
-        dx[:, T:, 0].copy_(dpk)                                         # (PK maps: Cf == 1)
         return dx
 
     def _pk_fusion_backward(self, S, k, de: Feat, gv):
@@ -782,7 +781,7 @@ class STFProgram:
         dpk = new_feat(pkb.N, pkb.H, pkb.W, pkb.C, de.buf.device)
         w = nhwc.memset0(nhwc.empty((C, pkb.C, 1, 1), torch.float32, de.buf.device))
         nhwc.copy_rows(fus.weight.detach(), cin, w, pkb.C, C, cin)
-        nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0)
+        nhwc.conv_dgrad(de, w, dpk, 1, 1, 1, 0, cache=False)
         if self.want_dx:                  # the resized PK maps' share, for _input_grad
             S.dpk_parts.append(dpk)
         return dpk.slice(0, C)

@@ -109,7 +109,7 @@ class DoubleConvProgram:
             wp = nhwc.memset0(nhwc.empty((self.cout, s.src.C, 3, 3), torch.float32, w1.device))
             nhwc.copy_rows(w1.detach(), cin * 9, wp, s.src.C * 9, self.cout, cin * 9)
             w1 = wp
-        nhwc.conv_dgrad(dy1, w1, dsrc, 3, 3, 1, 1)
+        nhwc.conv_dgrad(dy1, w1, dsrc, 3, 3, 1, 1, cache=w1 is conv1.weight)
         return dsrc
 
     def _wgrad_conv1(self, dy1, src, out):

@@ -501,11 +501,15 @@ def test_stf_eval_mode_backward_vs_oracle():
     assert not bad, bad
 
 
-def test_stf_input_gradient_vs_oracle():
+@pytest.mark.parametrize("train", [False, True])
+def test_stf_input_gradient_vs_oracle(train):
     """x.requires_grad: the input sequence's gradient (reference autograd returns it,
     src/stf_lstm_unet.py:139-256) -- the eager forward, then the stem's stf_stem_dgrad7 after the
-    backward -- vs autograd of the fp32 oracle in eval mode (within 2x the bf16 emulation's error +
-    0.02, as the parameter gradients above); the parameter gradients are those of the plain call."""
+    backward -- vs autograd of the fp32 oracle in eval and in training mode (within 2x the bf16
+    emulation's error + 0.02, as the parameter gradients above); the parameter gradients and, in
+    training mode, the BatchNorm running statistics and num_batches_tracked are those of the plain
+    call (the eager forward advances them exactly once); N such backwards leave the weight-pack
+    cache at a constant size (no per-call temporaries cached)."""
     import oracle.unet_bf16 as o_q
     from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
     from oracle.init import canonical_state_dict
@@ -515,30 +519,46 @@ def test_stf_input_gradient_vs_oracle():
     m = STFLSTMUNet(time_steps=4)
     sd = canonical_state_dict(m.state_dict(), seed=0)
     m.load_state_dict(sd)
-    m = m.to(DEV).eval()
+    m = m.to(DEV).train(train)
     x, t = torch.from_numpy(g["x"]), torch.from_numpy(g["target"])
     p = {k: v.clone() for k, v in sd.items()}
     xo = x.clone().requires_grad_(True)
-    o_loss.criterion(o_stf.forward(p, xo, False)["out"], t).backward()
+    o_loss.criterion(o_stf.forward(p, xo, train)["out"], t).backward()
     xe = x.clone().requires_grad_(True)
     with o_q.storage(torch.bfloat16):
-        o_loss.criterion(o_emu.forward(p, xe, False)["out"], t).backward()
+        o_loss.criterion(o_emu.forward(p, xe, train)["out"], t).backward()
     xh = x.to(DEV).requires_grad_(True)
     criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
     assert xh.grad is not None and xh.grad.shape == x.shape and torch.isfinite(xh.grad).all()
     e_hip, e_emu = rel(xh.grad, xo.grad), rel(xe.grad, xo.grad)
     assert e_hip < 2 * e_emu + 0.02, (e_hip, e_emu)
     grads = {k: v.grad.clone() for k, v in m.named_parameters()}
+    bufs = {k: v.clone() for k, v in m.state_dict().items() if "running" in k or "num_batches" in k}
+    m.load_state_dict(sd)
     m.zero_grad(set_to_none=True)
     criterion({"out": m(x.to(DEV))["out"]}, t.to(DEV)).backward()      # the planned path, no input grad
     for k, v in m.named_parameters():
         assert torch.equal(v.grad, grads[k]), k
+    for k, v in m.state_dict().items():
+        if k in bufs:
+            assert torch.equal(v, bufs[k]), k
+    n_packs = None
+    for _ in range(3):
+        m.zero_grad(set_to_none=True)
+        xh = x.to(DEV).requires_grad_(True)
+        criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
+        n = len(m.program.packs.bufs)
+        assert n_packs is None or n == n_packs, (n, n_packs)
+        n_packs = n
 
 
-def test_stf_input_gradient_pk_vs_oracle():
+@pytest.mark.parametrize("train", [False, True])
+def test_stf_input_gradient_pk_vs_oracle(train):
     """The same with PK maps on the T axis (x [B, T + 3, 1, H, W]): the frames' gradient from the
     stem, the PK maps' from the stem (every frame reads them) plus the four fusion branches through
-    the bilinear resize's backward, summed over the frames -- vs autograd of the fp32 oracle."""
+    the bilinear resize's backward, summed over the frames -- vs autograd of the fp32 oracle, eval
+    and training mode; the fusion branches' zero-padded dgrad weights are per-call temporaries that
+    must not accumulate in the weight-pack cache."""
     import oracle.unet_bf16 as o_q
     from oracle import loss as o_loss, stf as o_stf, stf_bf16 as o_emu
     from oracle.init import canonical_state_dict
@@ -547,22 +567,30 @@ def test_stf_input_gradient_pk_vs_oracle():
     m = STFLSTMUNet(time_steps=3, use_pk_maps=True)
     sd = canonical_state_dict(m.state_dict(), seed=1)
     m.load_state_dict(sd)
-    m = m.to(DEV).eval()
+    m = m.to(DEV).train(train)
     gen = torch.Generator().manual_seed(5)
     x = torch.rand(2, 6, 1, 96, 64, generator=gen)
     t = torch.randint(0, 2, (2, 48, 32), generator=gen)
     p = {k: v.clone() for k, v in sd.items()}
     xo = x.clone().requires_grad_(True)
-    o_loss.criterion(o_stf.forward(p, xo, False, use_pk_maps=True)["out"], t).backward()
+    o_loss.criterion(o_stf.forward(p, xo, train, use_pk_maps=True)["out"], t).backward()
     xe = x.clone().requires_grad_(True)
     with o_q.storage(torch.bfloat16):
-        o_loss.criterion(o_emu.forward(p, xe, False, use_pk_maps=True)["out"], t).backward()
+        o_loss.criterion(o_emu.forward(p, xe, train, use_pk_maps=True)["out"], t).backward()
     xh = x.to(DEV).requires_grad_(True)
     criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
     assert xh.grad is not None and xh.grad.shape == x.shape and torch.isfinite(xh.grad).all()
     for sl in (slice(0, 3), slice(3, 6)):                  # frames, PK maps
         e_hip, e_emu = rel(xh.grad[:, sl], xo.grad[:, sl]), rel(xe.grad[:, sl], xo.grad[:, sl])
         assert e_hip < 2 * e_emu + 0.02, (sl, e_hip, e_emu)
+    n_packs = None
+    for _ in range(3):
+        m.zero_grad(set_to_none=True)
+        xh = x.to(DEV).requires_grad_(True)
+        criterion({"out": m(xh)["out"]}, t.to(DEV)).backward()
+        n = len(m.program.packs.bufs)
+        assert n_packs is None or n == n_packs, (n, n_packs)
+        n_packs = n
 
 
 @pytest.mark.parametrize("B,T,Cf,H,W", [(2, 3, 1, 45, 38), (1, 2, 3, 64, 33), (1, 1, 6, 32, 32)])

@@ -49,7 +49,7 @@ def test_library_exports_every_header_symbol(dtype):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/stfunet.h but not exported"
     assert set(syms) == set(_lib.EXPORTED)
-    assert lib.stf_abi_version() == 16
+    assert lib.stf_abi_version() == 17
     assert lib.stf_storage_type() == _lib.STORAGE_CODE[dtype]
     assert b"invalid argument" in lib.stf_error_string(100001)
 

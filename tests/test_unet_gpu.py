@@ -351,6 +351,14 @@ def test_unet_input_gradient_vs_oracle(train, cin):
     criterion({"out": model(x.to(DEV))["out"]}, t.to(DEV)).backward()
     for k, v in model.named_parameters():
         assert torch.equal(v.grad, g_with[k]), k
+    n_packs = None          # per-call zero-padded dgrad weights stay out of the pack cache
+    for _ in range(3):
+        model.zero_grad()
+        xg = x.to(DEV).requires_grad_()
+        criterion({"out": model(xg)["out"]}, t.to(DEV)).backward()
+        n = len(model.program.packs.bufs)
+        assert n_packs is None or n == n_packs, (n, n_packs)
+        n_packs = n
 
 
 def test_gradient_accumulation_without_zero_grad():
