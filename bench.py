@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--hook", action="store_true",
                     help="N = 1: form a world-1 RCCL group and attach the data-parallel gradient hook "
                          "(stfunet.ddp.GradAllReduce), i.e. time the per-GPU half of the DP step")
+    ap.add_argument("--contend", default=None, metavar="BLOCKS,GBPS",
+                    help="with --hook: after each bucket's collective, a proxy of what an 8-GPU RCCL "
+                         "all-reduce does to the compute stream's CUs -- BLOCKS resident workgroups for "
+                         "2*7/8*bytes/GBPS on the joiner stream (tools/contend); e.g. 32,300")
     a = ap.parse_args()
     presets = {2: dict(model="unet", batch=64, size=256, time_steps=8, pk=False, dtype="bf16"),
                3: dict(model="stf", batch=16, size=256, time_steps=8, pk=False, dtype="bf16"),
@@ -382,6 +386,8 @@ def main():
     steps_total = args.warmup + args.steps
     sched = engine.create_lr_scheduler(opt, max(steps_total, 1), 10, warmup=True)
     ddp = GradAllReduce(model) if dist_on else None
+    if args.contend and ddp is not None:
+        ddp.after_launch = _contend_proxy(args.contend, dev)
 
     # synthetic batches resident in HBM before the timed region
     half = (args.size // 2, args.size // 2) if args.model == "stf" else None   # STF predicts at H/2
@@ -500,7 +506,7 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": args.time_steps, "image": [args.size, args.size],
                        "parallelism": f"dp{world}", "ddp_hook": bool(ddp is not None)},
-            **({"rccl_stream": rccl_stream_note()} if ddp is not None else {}),
+            **({"rccl_stream": rccl_stream_note(), "contend": args.contend} if ddp is not None else {}),
             "train_gflop_per_sample": round(train_gflop, 2),
             "model_tflops_per_gpu": round(value / world * train_gflop / 1e3, 2),
             "model_mfu": round(value / world * train_gflop / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
@@ -509,6 +515,7 @@ def main():
             "kernels_census_step": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in d.items()}
                                     for k, d in census.items()},
             "last_loss": round(last_loss, 5),
+            "build": _build_record(),
         }
         if not args.no_dice and world == 1:    # evaluate() all-reduces: rank 0 alone must not call it at N > 1
             res["dice_vs_ref"] = (dice_vs_reference(dev, args.dtype) if args.model == "unet"
@@ -535,6 +542,35 @@ def main():
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _contend_proxy(spec, dev):
+    """bench-only: tools/contend/libcontend.so's RCCL-shaped occupancy kernel, launched on the
+    joiner stream right after each bucket's collective (see --contend)."""
+    import ctypes
+    blocks, gbps = (float(v) for v in spec.split(","))
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "contend", "libcontend.so"))
+    lib.contend_launch.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
+    scratch = {}
+
+    def launch(t):
+        nbytes = t.numel() * t.element_size()
+        buf = scratch.get(nbytes)
+        if buf is None:
+            buf = scratch[nbytes] = torch.zeros(nbytes // 4, dtype=torch.float32, device=dev)
+        usec = 2 * 7 / 8 * nbytes / (gbps * 1e9) * 1e6
+        rc = lib.contend_launch(buf.data_ptr(), nbytes, int(blocks), usec,
+                                torch.cuda.current_stream(dev).cuda_stream)
+        assert rc == 0, rc
+    return launch
+
+
+def _build_record():
+    """Which build ran: the loaded libraries' digests and the source digest they were built from
+    (__graft_entry__.build() records it next to them)."""
+    from stfunet import _lib
+    i = _lib.build_info()
+    return {"src": i["src_recorded"], "src_now": i["src_now"], "lib": i["lib"], "current": i["current"]}
 
 
 if __name__ == "__main__":

@@ -1662,14 +1662,352 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo2_kernel(Geo a, uint32_t s
   halo_body<16, 32, 8, 2, 0, DIRECT, BNR, 2, DEFER>(a, src_bytes, TY, TX, per, rem);
 }
 
-// four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves.  ST = 1: one stage, two
-// workgroups per CU (61 KB of LDS each) -- one workgroup's DMA waits hide behind the other's
-// MFMAs; ST = 2: a 2-stage ring, one workgroup per CU (123 KB), for grids that would not put two
-// workgroups on every CU (STF cfg3: 256 items)
-template <int DIRECT, int ST>
-__global__ __launch_bounds__(256, ST == 1 ? 2 : 1) void conv3x3_halo4_kernel(Geo a, uint32_t src_bytes, int TY,
-                                                                             int TX, int per, int rem) {
-  halo_body<8, 32, 4, ST, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
+// four 8 x 8 images per 8 x 32 tile (IX = 4; STF layer4), 4 waves, one stage, two workgroups per
+// CU (61 KB of LDS each): one workgroup's DMA waits hide behind the other's MFMAs.  (A 2-stage
+// ring at one workgroup per CU, for grids under 2 x CUs, was faster alone -- forward 64 -> 61 us,
+// BN-backward dgrad 84 -> 66 us -- but its 123 KB of LDS kept the side streams' weight gradients
+// and LSTMs off the CU: the STF step -0.5 % over five same-box repeats; removed in round 6.)
+template <int DIRECT>
+__global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
+                                                               int rem) {
+  halo_body<8, 32, 4, 1, 0, DIRECT, false, 4>(a, src_bytes, TY, TX, per, rem);
+}
+
+// ---------------------------------------------------------------------------
+// Wide halo kernel (round 6): the same 3x3 / stride 1 / pad 1 convolution as halo_body, for layers
+// with >= 128 output channels, with a 16 x 32 pixel tile x 128-channel output slice per item
+// (twice the outputs per workgroup: 128 accumulator registers per lane, wave tile 64 pixels x 128
+// channels).  Per 32-channel source chunk (one "stage") the workgroup needs the (16+2) x (32+2)
+// halo (39 KB, as halo_body) and 9 x 128 weight rows (74 KB): the same halo bytes for twice the
+// MFMAs, 26 % fewer LDS-fill bytes per FLOP than the 64-channel slice.  Two whole stages do not
+// fit in 160 KiB, so the weights are not double-buffered by stage: they live in two tap-group
+// buffers (G0 = taps 0-4, G1 = taps 5-8), each refilled as soon as every wave has finished its taps
+// -- G0 of the next chunk streams in while G1 of this chunk computes.  One barrier per group
+// ("point"; a 3-group variant measured 1-2 % slower per layer):
+//   P0(s): wait halo(s) + G0(s);  issue G1(s), halo(s+1)   [then taps 0-4 from G0]
+//   P1(s): wait G1(s);            issue G0(s+1)            [taps 5-8 from G1]
+// (the weights are L2-resident: 4-5 taps of MFMAs cover their fill; the halo has a whole stage).
+// Every wave issues the same count at every point (4 + 5 and 5 DMA instructions, past the last
+// stage with all lanes out of range), so the waits are fixed vmcnt values.  The first tap of G1
+// reads its halo fragments before the P1 barrier.  Waves 4..7 (the SIMD partners of 0..3)
+// issue their share after the first tap's first MFMA block, so the two waves of a SIMD do not
+// stall on LDS-DMA issue together.  Direct epilogue (16-B stores of 8 consecutive channels,
+// weight rows fetched in the permuted order of halo_body's DIRECT), BatchNorm partial statistics
+// as halo_body's non-deferred path (one row per (group, workgroup)), the slice's biases by one
+// LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad).
+#ifndef WIDE_STAGGER
+#define WIDE_STAGGER 0
+#endif
+namespace wide {
+constexpr int NW = 8, PH = 16, PW = 32, BN = 128, RPI = 16;
+constexpr int HW = PW + 2, HR = (PH + 2) * HW;          // 612 halo rows
+constexpr int HIN = 40, HPW = HIN / NW;                 // halo DMA instructions per stage: 5 per wave
+constexpr int HSTAGE = HIN * RPI * 64;                  // 40960 B (rows >= 612 stay zero, never read)
+// two weight groups per stage: G0 = taps 0-4 (640 rows, 5 DMA instructions per wave), G1 = taps 5-8
+// (512 rows, 4 per wave)
+constexpr int G1T = 5;                                  // first tap of G1
+constexpr int GPW0 = G1T * BN / RPI / NW, GPW1 = (9 - G1T) * BN / RPI / NW;
+constexpr int G0BYTES = G1T * BN * 64;                  // 40960 B
+constexpr int WOFF = 2 * HSTAGE;                        // 81920: G0, then G1 at WOFF + G0BYTES
+constexpr int BOFF = WOFF + 9 * BN * 64;                // 155648: the slice's 128 biases (1 KiB DMA target)
+constexpr int ROFF = BOFF + 1024;                       // 156672: running statistics partials [2][128] fp32
+constexpr int LDS = ROFF + 1024;                        // 157696
+constexpr int TM = 4, TN = 8, NST = 2 * TN;             // 16 epilogue stores per lane
+static_assert(HIN * RPI >= HR && HIN % NW == 0 && G1T * BN % (RPI * NW) == 0 && (9 - G1T) * BN % (RPI * NW) == 0,
+              "wide halo geometry");
+static_assert(NW * 2 * BN * 4 <= (9 - G1T) * BN * 64, "statistics scratch in the G1 weight buffer");
+}
+
+template <int DIRECT>
+__global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
+                                                              int rem) {
+  using namespace wide;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fk = lane >> 4, sub = lane >> 2, slot = lane & 3;
+  const int NTn = a.Nout / BN, CC = a.Cs / 32, tpi = TY * TX;
+  const int ntiles = a.N * tpi;
+  const int ipg = a.Mg / (a.Hd * a.Wd);
+  const int vb = blockIdx.x;
+  const int cnt = per + (int)(vb < rem);
+  const int it0 = vb * per + min(vb, rem);
+  const int S = cnt * CC;
+  const bool has_bias = DIRECT == 2 && a.bias != nullptr;
+  const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_wgt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, 0, (uint32_t)a.Nout * a.K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_bias =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, a.bias ? (uint32_t)a.Nout * 4 : 0u, 0x00020000);
+  constexpr uint32_t BAD = 0xFFFFFFF0u;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+
+  // stage s = (item it0 + s / CC, chunk s % CC); s >= S: not live (all lanes out of range)
+  auto issue_halo = [&](int s) {
+    const bool live = s < S;
+    const int item = it0 + (live ? s / CC : 0), cc = live ? s % CC : 0;
+    const int tile = item % ntiles;
+    const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+    const int y0 = ty * PH - 1, x0 = tx * PW - 1;
+    char* st = smem + (s & 1) * HSTAGE;
+    // the lane's row terms are recomputed at every issue (opaque copy): kept live across the taps
+    // they would cost ~20 registers that the accumulators need
+    int sb = sub;
+    asm volatile("" : "+v"(sb));
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int hr = (wave * HPW + i) * RPI + sb;
+      const int hy = hr / HW, hx = hr - hy * HW;
+      const int ys = y0 + hy, xs = x0 + hx;
+      const bool ok = live && hr < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws;
+      const uint32_t off =
+          ok ? (uint32_t)((((img * a.Hs + ys) * a.Ws + xs) * a.scs + cc * 32 + swzh(hx, slot) * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_src, (lds_ptr)(st + (wave * HPW + i) * RPI * 64), 16, off, 0, 0, 0);
+    }
+  };
+  // weight rows of tap group g of stage s into its buffer: row (tap - first tap) * 128 + wrow
+  auto issue_w = [&](int s, auto gc) {
+    constexpr int g = decltype(gc)::value, GPW = g ? GPW1 : GPW0;
+    const bool live = s < S;
+    const int item = it0 + (live ? s / CC : 0), cc = live ? s % CC : 0;
+    const int nt = item / ntiles;
+    char* wb = smem + WOFF + g * G0BYTES;
+    int sb = sub;
+    asm volatile("" : "+v"(sb));
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+      const int wr = (wave * GPW + i) * RPI + sb;
+      const int wrow = wr & (BN - 1), tap = g * G1T + wr / BN;
+      const int n = nt * BN + (wrow >> 5) * 32 + ((wrow >> 2) & 3) * 8 + ((wrow >> 4) & 1) * 4 + (wrow & 3);
+      const uint32_t off = live ? (uint32_t)(((size_t)n * a.K + tap * a.Cs + cc * 32 + swzh(wr, slot) * 8) * 2) : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_wgt, (lds_ptr)(wb + (wave * GPW + i) * RPI * 64), 16, off, 0, 0, 0);
+    }
+  };
+  // wave 0, first chunk of an item: the slice's 128 biases (lanes 0..31 x 16 B) into BOFF
+  auto issue_bias = [&](int s) {
+    const int nt = (it0 + s / CC) / ntiles;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t off = ln < BN / 4 ? (uint32_t)((nt * BN + ln * 4) * 4) : BAD;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_bias, (lds_ptr)(smem + BOFF), 16, off, 0, 0, 0);
+  };
+
+  // this lane's halo read address for tap column dx (fragment 0, tap row 0, stage 0).  Fragment i
+  // is pixel row 2*wave + (i >> 1), columns (i & 1) * 16 + fr: both shifts leave the column-keyed
+  // swizzle unchanged (key hx + 16 flips no bit of (hx >> 1) & 2), so fragment, tap row and ring
+  // stage are all immediate offsets -- three address registers in all
+  const uint32_t s32 = (uint32_t)(uintptr_t)(lds_ptr)smem;
+  uint32_t xa[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int hx = fr + dx;
+    xa[dx] = s32 + (uint32_t)(((2 * wave) * HW + hx) * 64 + swzh(hx, fk) * 16);
+  }
+  // weight rows: G0 from wb0, G1 from wb1 (immediate offsets < 40 KiB)
+  const uint32_t wb0 = s32 + (uint32_t)(WOFF + fr * 64 + swzh(fr, fk) * 16);
+  const uint32_t wb1 = wb0 + G0BYTES;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // BatchNorm partial statistics rows [groups][gridDim][2][Nout], as halo_body (non-deferred): thread
+  // tid < 256 owns (sum | sum of squares, channel) tid of the current (group, slice) key, its running
+  // value in LDS (ROFF) and its row addresses recomputed when used (registers go to the accumulators)
+  float* const sbuf = DIRECT == 2 ? a.stats : nullptr;
+  float* const runl = reinterpret_cast<float*>(smem + ROFF);
+  const int groups = a.M / a.Mg;
+  auto srow_ptr = [&](int key) {                        // (group, slice) key -> this thread's element
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    const int g = key / NTn, nt = key - g * NTn;
+    return sbuf + ((size_t)(g * gridDim.x + vb) * 2 + (t >> 7)) * a.Nout + nt * BN + (t & 127);
+  };
+  int run_key = -1;                                      // wave-uniform
+  if (sbuf && tid < 256) {
+    for (int k = 0; k < groups * NTn; ++k) *srow_ptr(k) = 0.f;
+  }
+
+  // prologue: the fills points P0(-1), P1(-1) would have issued
+  issue_halo(0);
+  issue_w(0, std::integral_constant<int, 0>());
+
+  e16x8 xf[2][TM], wf[TN];
+  auto rdA = [&](int t, int b, int ph) {                // ph: ring stage (compile-time)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(xf[b][i])
+                   : "v"(xa[t % 3]), "i"(ph * HSTAGE + (t / 3 + (i >> 1)) * HW * 64 + (i & 1) * 16 * 64));
+  };
+  auto rdB = [&](int t, int half) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = half * 4 + jj;
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(wf[j]) : "v"(t >= G1T ? wb1 : wb0), "i"(((t >= G1T ? t - G1T : t) * BN + j * 16) * 64));
+    }
+  };
+  bool epi = false;
+  int cc = 0, item = it0;
+  // two stages per iteration, so the ring stage of every LDS read is an immediate
+  for (int s2 = 0; s2 < S; s2 += 2)
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    const int s = s2 + ph;
+    if (s >= S) break;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int t0 = g ? G1T : 0, t1 = g ? 9 : G1T;
+      // ---- point P_g(s): this wave's fills for it have landed, then the barrier publishes everyone's
+      // (and every wave has finished reading the buffer the point's fills overwrite)
+      if (g == 0) {
+        if (epi) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NST) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        epi = false;
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(HPW) : "memory");   // (halo(s+1) may stay in flight)
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      auto issue_point = [&]() {
+        if (g == 0) {
+          if (has_bias && cc == 0 && wave == 0) issue_bias(s);
+          issue_w(s, std::integral_constant<int, 1>());
+          issue_halo(s + 1);
+        } else {
+          issue_w(s + 1, std::integral_constant<int, 0>());
+        }
+      };
+      if (WIDE_STAGGER == 0 || wave < NW / 2) issue_point();   // (stagger: waves 4..7 after their first MFMA block)
+      // ---- taps t0 .. t1-1, software-pipelined: A of tap t+1 (also across the group boundary: the
+      // halo is the stage's) and each half of B of tap t+1 (within the group) are read while tap t's
+      // MFMAs run
+      if (g == 0) rdA(0, 0, ph);
+      rdB(t0, 0);
+      rdB(t0, 1);
+#pragma unroll
+      for (int t = t0; t < t1; ++t) {
+        const int b = t & 1;
+        const bool nA = t + 1 < 9, nB = t + 1 < t1;
+        if (nA) rdA(t + 1, b ^ 1, ph);
+        if (nA)
+          asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(xf[b][0]), "+v"(xf[b][1]), "+v"(xf[b][2]), "+v"(xf[b][3]),
+                       "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xf[b][0]), "+v"(xf[b][1]), "+v"(xf[b][2]), "+v"(xf[b][3]),
+                       "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]));
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[i][jj] = mfma16x16x32(wf[jj], xf[b][i], acc[i][jj]);
+        if (WIDE_STAGGER && t == t0 && wave >= NW / 2) issue_point();
+        if (nB) {
+          rdB(t + 1, 0);
+          asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(wf[4]), "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
+        } else if (nA) {
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(wf[4]), "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[4]), "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
+        }
+#pragma unroll
+        for (int jj = 4; jj < 8; ++jj)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[i][jj] = mfma16x16x32(wf[jj], xf[b][i], acc[i][jj]);
+        if (nB) rdB(t + 1, 1);
+      }
+    }
+    if (++cc < CC) continue;
+    // ---- direct epilogue of `item`: lane (fr, fk) holds pixel i*16+fr, channels h*32 + fk*8 + 0..7
+    // in acc[i][2h], acc[i][2h+1]; every lane issues exactly NST stores (invalid pixels out of range)
+    cc = 0;
+    {
+      const int nt = item / ntiles, tile = item - nt * ntiles;
+      const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
+      const __amdgpu_buffer_rsrc_t rs_dst =
+          __builtin_amdgcn_make_buffer_rsrc((void*)a.dst, 0, (uint32_t)((size_t)a.M * a.dcs * 2), 0x00020000);
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      int mq[TM];
+      int fo = fr, ko = fk;                              // (opaque: recomputed per item, not kept live)
+      asm volatile("" : "+v"(fo), "+v"(ko));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int y = ty * PH + 2 * wave + (i >> 1), x = tx * PW + (i & 1) * 16 + fo;
+        mq[i] = (y < a.Hd && x < a.Wd) ? (img * a.Hd + y) * a.Wd + x : -1;
+      }
+      float res[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (has_bias) {
+          const float4 lo = *reinterpret_cast<const float4*>(smem + BOFF + (h * 32 + ko * 8) * 4);
+          const float4 hi = *reinterpret_cast<const float4*>(smem + BOFF + (h * 32 + ko * 8 + 4) * 4);
+          bb[0] = lo.x; bb[1] = lo.y; bb[2] = lo.z; bb[3] = lo.w; bb[4] = hi.x; bb[5] = hi.y; bb[6] = hi.z; bb[7] = hi.w;
+        }
+        float v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float f[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            f[r] = acc[i][2 * h][r] + bb[r];
+            f[4 + r] = acc[i][2 * h + 1][r] + bb[4 + r];
+          }
+          const uint32_t off =
+              mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.dcs + nt * BN + h * 32 + ko * 8) * 2) : BAD;
+          if (a.accumulate) {                            // (out-of-range lanes read zeros)
+            const u32x4 ov = __builtin_amdgcn_raw_buffer_load_b128(rs_dst, off, 0, 0);
+            float o[8];
+            unpack8(make_uint4(ov.x, ov.y, ov.z, ov.w), o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += o[e];
+          }
+          const uint4 u = pack8(f);
+          acc[i][2 * h] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc[i][2 * h + 1] = f32x4{0.f, 0.f, 0.f, 0.f};
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{u.x, u.y, u.z, u.w}, rs_dst, off, 0, 0);
+          if constexpr (DIRECT == 2) {
+            float gq[8];
+            unpack8(u, gq);
+            const float w = mq[i] >= 0 ? 1.f : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { v[e] += w * gq[e]; v[8 + e] += w * gq[e] * gq[e]; }
+          }
+        }
+        if constexpr (DIRECT == 2) res[h] = row16_reduce_scatter(v, fo);
+      }
+      epi = true;
+      if (sbuf) {
+        // every wave is done with the G1 buffer (its last taps): it holds the cross-wave partials
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        float* red = reinterpret_cast<float*>(smem + WOFF + G0BYTES);         // [NW][2][128]
+#pragma unroll
+        for (int h = 0; h < 4; ++h) red[(wave * 2 + (fo >> 3)) * BN + h * 32 + ko * 8 + (fo & 7)] = res[h];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int key = (img / ipg) * NTn + nt;
+        int to = tid;
+        asm volatile("" : "+v"(to));
+        if (to < 256) {
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += red[w * 2 * BN + to];
+          const float prev = runl[to];
+          if (key != run_key && run_key >= 0) *srow_ptr(run_key) = prev;
+          runl[to] = (key != run_key ? 0.f : prev) + t;
+        }
+        run_key = key;
+      }
+    }
+    ++item;
+  }
+  if (sbuf && tid < 256 && run_key >= 0) *srow_ptr(run_key) = runl[tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // the trailing (not live) fills have landed
 }
 
 // ---------------------------------------------------------------------------
@@ -1905,12 +2243,22 @@ int halo_ix(const stf_igemm_args* a, bool with_stats);
 int halo_grid(const stf_igemm_args* a, int ix);
 void halo_tiles(const stf_conv_geom& c, int& ty, int& tx);
 
+// the wide halo kernel (conv3x3_wide_kernel: 128-channel output slices) for 3x3 layers with >= 128
+// output channels and W >= 32, forward and plain dgrad (not the BN-backward-fused dgrad);
+// STF_HALO_WIDE=0: the 64-channel halo kernel (A/B)
+bool halo_wide(const stf_igemm_args* a) {
+  static const int on = stf::ab_switch("STF_HALO_WIDE", 1);
+  const stf_conv_geom& c = a->g;
+  return on && !a->bnr && !a->lstm && !a->scatter2x2 && !c.transposed && halo_direct(a) && a->Nout % 128 == 0 &&
+         c.Wd >= 32 && c.Cs % 32 == 0 && halo_ix(a, a->stats != nullptr) == 1;
+}
+
 // deferred epilogue of the second wave half (halo_body DEFER; default on, STF_HALO_DEFER=0: off, A/B).  Its
 // statistics fold keeps at most 2 (group, slice) keys per workgroup: the item run of a workgroup
 // (items / grid + 1, slice-major, image-major within a slice) must not span more.
 bool halo_defer(const stf_igemm_args* a) {
   static const int on = stf::ab_switch("STF_HALO_DEFER", 1);
-  if (!(on && halo_direct(a) && !halo8(a))) return false;
+  if (!(on && halo_direct(a) && !halo8(a)) || halo_wide(a)) return false;
   // (not the two-image 16 x 16 tiles: their deferred variants spill registers)
   const int ix = halo_ix(a, a->stats != nullptr);
   if (ix > 1) return false;
@@ -2111,25 +2459,13 @@ long halo_items_ix(const stf_igemm_args* a, int ix) {
   int ty, tx;
   halo_tiles(a->g, ty, tx);
   if (ix > 1) ty = tx = 1;
-  return (long)(a->g.N / ix) * ty * tx * (a->Nout / 64);
-}
-
-// stages of the 8 x 8 (IX = 4) halo kernel (STF_HALO4_ST=2: the 2-stage ring).  With fewer items
-// than 2 x CUs (STF cfg3: 256) the single-stage kernel runs one workgroup per CU with its DMA waits
-// exposed, and the 2-stage ring is faster alone (census: forward 64 -> 61 us, BN-backward dgrad
-// 84 -> 66 us) -- but in the step, beside the side streams' weight gradients and LSTMs that its
-// 123 KB of LDS keeps off the CU, it measured -0.5 % on average over five same-box repeats, so
-// the single-stage kernel stays the default
-int halo4_stages(const stf_igemm_args* a) {
-  static const int force = stf::ab_switch("STF_HALO4_ST", 1);
-  (void)a;
-  return force == 2 ? 2 : 1;
+  return (long)(a->g.N / ix) * ty * tx * (a->Nout / (ix == 1 && halo_wide(a) ? 128 : 64));
 }
 
 // persistent halo grid: one workgroup per CU (160 KiB LDS each; the single-stage 8 x 8 kernel two)
 int halo_grid(const stf_igemm_args* a, int ix) {
   const long items = halo_items_ix(a, ix);
-  return (int)std::min<long>(items, (long)num_cus() * (ix == 4 && halo4_stages(a) == 1 ? 2 : 1));
+  return (int)std::min<long>(items, (long)num_cus() * (ix == 4 ? 2 : 1));
 }
 
 // Split-K factor for a plain gather on the linear DMA kernels that would leave the
@@ -2198,7 +2534,9 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
     case 'K': snprintf(buf, sizeof buf, "conv3x3_c8_kernel"); break;
     case 'H':
       if (halo8(a))
-        snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0, %d>", halo4_stages(a));
+        snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
+      else if (halo_wide(a))
+        snprintf(buf, sizeof buf, "conv3x3_wide_kernel<%d>", a->stats ? 2 : 1);
       else if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false", halo_defer(a) ? "true" : "false");
@@ -2312,7 +2650,7 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     halo_tiles(c, ty, tx);
     const int ix = halo_ix(a, a->stats != nullptr);
     if (ix > 1) ty = tx = 1;
-    const long items = (long)(c.N / ix) * ty * tx * (a->Nout / 64);
+    const long items = halo_items_ix(a, ix);
     const int grid = halo_grid(a, ix);
     static const int diag = stf::ablation_env("STF_HALO_DIAG");
 #define STF_H(D) hipLaunchKernelGGL((conv3x3_halo_kernel<16, HALO_PW, 8, 2, D>), dim3(grid), dim3(512), 0, s, g, \
@@ -2332,11 +2670,11 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
       else hipLaunchKernelGGL((conv3x3_halo2_kernel<D, B>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per,   \
                               rem);                                                                                    \
     } while (0)
-    if (ix == 4) {
-      if (halo4_stages(a) == 2)
-        hipLaunchKernelGGL((conv3x3_halo4_kernel<0, 2>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
-      else
-        hipLaunchKernelGGL((conv3x3_halo4_kernel<0, 1>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
+    if (ix == 1 && halo_wide(a)) {
+      if (d == 2) hipLaunchKernelGGL((conv3x3_wide_kernel<2>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per, rem);
+      else hipLaunchKernelGGL((conv3x3_wide_kernel<1>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per, rem);
+    } else if (ix == 4) {
+      hipLaunchKernelGGL((conv3x3_halo4_kernel<0>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);
     } else if (ix > 1) {
       if (bnr_fused(a, k)) STF_H2(1, true);
       else if (d == 2) STF_H2(2, false);

@@ -479,145 +479,6 @@ __global__ __launch_bounds__(NT, 2) void wgrad3x3_c8_kernel(WArgs a, int tiles_y
     slab[i] = (red[i] + red[64 * 72 + i]) + (red[2 * 64 * 72 + i] + red[3 * 64 * 72 + i]);
 }
 
-// ---------------------------------------------------------------------------
-// The same fused-tap weight gradient with LDS-DMA staging: dy tile and x halo go
-// global -> LDS by `buffer_load ... lds` (no register staging, no ds_write), in a
-// 3-stage ring with two tiles in flight.  Rows are 128 B (64 channels); the 16-B
-// chunk c of a row whose pixel has x coordinate (within the tile / halo) xx sits at
-// slot c ^ (xx & 7).  The eight rows a 32-lane half reads with ds_read_b64_tr_b16
-// are eight consecutive x of one image row, so they cover all 64 banks once
-// (conflict-free) without padding, and each DMA instruction fills 8 whole rows
-// (1 KiB).  Keying on x (not on the row index) keeps the tap's row shift dy and the
-// k-step out of the swizzle: those become immediate offsets, and a lane needs only
-// 4 + 6 address registers (A per fragment i, B per (h, dx)).  Per tile 24 DMA
-// instructions (8 dy + 16 halo, the halo rounded up to 128 rows): 6 per wave, the
-// same count every iteration (a tile past the end is issued with every lane out of
-// range, which writes zeros into a buffer nobody reads), so `vmcnt(6)` retires
-// exactly the tile about to be read.
-template <int PW>
-__global__ __launch_bounds__(NT, 2) void wgrad3x3_dma_kernel(WArgs a, int tiles_y, int tiles_x, int ntiles,
-                                                              uint32_t dy_bytes, uint32_t x_bytes) {
-  constexpr int PH = 64 / PW, HW = PW + 2, HR = (PH + 2) * HW;
-  constexpr int AR = 64, BR = 128, NA = AR / 8, NB = BR / 8, PERW = (NA + NB) / 4;
-  constexpr int STAGE = (AR + BR) * 128, STAGES = 3;
-  static_assert(HR <= BR && (NA + NB) % 4 == 0 && NT == 256 && PW % 8 == 0, "tile");
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar DMA addressing
-  constexpr int TMW = 4;                        // wave: all 64 dy channels x its 16 x channels x 9 taps
-  const int wn = wave;
-  const int split = blockIdx.x;
-  const int n0 = blockIdx.y * 64, c0 = blockIdx.z * 64;
-  const int t_begin = split * a.chunk, t_end = min(ntiles, t_begin + a.chunk);
-  const int per_img = tiles_y * tiles_x;
-  const __amdgpu_buffer_rsrc_t rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, dy_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, x_bytes, 0x00020000);
-  constexpr uint32_t BAD = 0xFFFFFFF0u;
-
-  auto issue = [&](int t, int buf, bool live) {
-    const int img = t / per_img, rem = t - img * per_img;
-    const int ty = rem / tiles_x, tx = rem - ty * tiles_x;
-    const int y0 = ty * PH, x0 = tx * PW;
-    char* st = smem + buf * STAGE;
-#pragma unroll
-    for (int k = 0; k < PERW; ++k) {
-      const int ins = wave * PERW + k;         // wave-uniform
-      const int r8 = lane >> 3;
-      uint32_t off = BAD;
-      if (ins < NA) {
-        const int px = ins * 8 + r8, yy = px / PW, xx = px % PW, yd = y0 + yy, xd = x0 + xx;
-        const int c = (lane & 7) ^ (xx & 7);
-        if (live && yd < a.Hd && xd < a.Wd)
-          off = (uint32_t)((((size_t)(img * a.Hd + yd) * a.Wd + xd) * a.dycs + n0 + c * 8) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs_dy, (__attribute__((address_space(3))) void*)(st + ins * 1024), 16, off, 0, 0, 0);
-      } else {
-        const int hp = (ins - NA) * 8 + r8, hy = hp / HW, hx = hp - hy * HW, ys = y0 - 1 + hy, xs = x0 - 1 + hx;
-        const int c = (lane & 7) ^ (hx & 7);
-        if (live && hp < HR && ys >= 0 && xs >= 0 && ys < a.Hs && xs < a.Ws)
-          off = (uint32_t)((((size_t)(img * a.Hs + ys) * a.Ws + xs) * a.xcs + c0 + c * 8) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs_x, (__attribute__((address_space(3))) void*)(st + ins * 1024), 16, off, 0, 0, 0);
-      }
-    }
-  };
-
-  f32x4 acc[9][TMW];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int i = 0; i < TMW; ++i) acc[t][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // lane (g, q, p4): k-slot 8g + 4h + q (h = lo/hi read) holds pixel
-  // px = 32 k2 + 8 h + pl of the tile, pl = 16(g>>1) + 4(g&1) + q (as in wgrad3x3_kernel).
-  // A row = px: x & 7 = pl & 7 for every (k2, h); row offset (32 k2 + 8 h) * 128 immediate.
-  // B row = AR + (px / PW + dy) * HW + px % PW + dx: x & 7 = (pl + dx) & 7; k2 moves 32 / PW
-  // image rows and dy one (immediates); h can carry into the next image row (register).
-  const int g = lane >> 4, q = (lane >> 2) & 3, p4 = (lane & 3) * 4;
-  const int pl = 16 * (g >> 1) + 4 * (g & 1) + q;
-  const int sub = (p4 & 7) * 2;                 // byte within the 16-B chunk
-  int aoff[TMW], boff[2][3];
-#pragma unroll
-  for (int i = 0; i < TMW; ++i) aoff[i] = pl * 128 + (((2 * i + (p4 >> 3)) ^ (pl & 7)) << 4) + sub;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
-      const int px = 8 * h + pl;
-      const int row = AR + (px / PW) * HW + px % PW + dx;
-      boff[h][dx] = row * 128 + (((2 * wn + (p4 >> 3)) ^ ((px % PW + dx) & 7)) << 4) + sub;
-    }
-
-  const int steps = t_end - t_begin;
-  issue(t_begin, 0, steps > 0);
-  issue(t_begin + 1, 1, steps > 1);
-  for (int it = 0; it < steps; ++it) {
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PERW) : "memory");   // this tile landed (own part)
-    __builtin_amdgcn_s_barrier();               // all parts landed; every wave is done with tile it-1
-    issue(t_begin + it + 2, (it + 2) % STAGES, it + 2 < steps);
-    const char* st = smem + (it % STAGES) * STAGE;
-    auto rd = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(st + off)); };
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      e16x8 af[TMW];
-#pragma unroll
-      for (int i = 0; i < TMW; ++i) {
-        v4s lo = rd(aoff[i] + (32 * k2) * 128);
-        v4s hi = rd(aoff[i] + (32 * k2 + 8) * 128);
-        short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(e16x8, s8);
-      }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int dy = t / 3, dx = t % 3;
-        const int imm = ((32 / PW) * k2 + dy) * HW * 128;
-        v4s lo = rd(boff[0][dx] + imm);
-        v4s hi = rd(boff[1][dx] + imm);
-        short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const e16x8 bfr = __builtin_bit_cast(e16x8, s8);
-#pragma unroll
-        for (int i = 0; i < TMW; ++i)
-          acc[t][i] = mfma16x16x32(af[i], bfr, acc[t][i]);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (dummy) DMAs
-
-  const int RSC = 9 * a.Cs;
-  float* out = a.ws + (size_t)(a.one_slab ? 0 : split) * a.Nout * RSC;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int i = 0; i < TMW; ++i) {
-      const int k = t * a.Cs + c0 + wn * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + i * 16 + (lane >> 4) * 4 + r;
-        out[(size_t)n * RSC + k] = acc[t][i][r];
-      }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // ConvTranspose2d(k=2, s=2) weight gradient: one block per (64 dy-channel,
@@ -848,15 +709,6 @@ int fused_pw(const stf_wgrad_args* a) {
   return c.Wd >= 16 ? 16 : 8;
 }
 
-// LDS-DMA staging for the fused 3x3 kernel (STF_WGRAD_DMA=0: register staging, A/B);
-// buffer offsets are 32-bit
-bool wgrad_dma(const stf_wgrad_args* a) {
-  static const bool on = stf::ab_switch("STF_WGRAD_DMA", 0) == 1;
-  const stf_conv_geom& c = a->g;
-  return on && (uint64_t)c.N * c.Hd * c.Wd * a->dy_cstride * 2 < 0xFFFFFF00ull &&
-         (uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2 < 0xFFFFFF00ull;
-}
-
 // ConvT 2x2 / stride 2 fused-tap kernel (x = the 2x larger gradient tensor)
 int fused22_pw(const stf_wgrad_args* a) {
   static const bool enabled = stf::ab_switch("STF_WGRAD_FUSED", 1) != 0;
@@ -948,7 +800,6 @@ extern "C" int stf_wgrad_plan(const stf_wgrad_args* a, int* splits, size_t* ws_b
 extern "C" const char* stf_wgrad_kernel_name(const stf_wgrad_args* a) {
   if (fused_c8(a)) return "wgrad3x3_c8_kernel";
   if (const int pw = fused_pw(a)) {
-    if (wgrad_dma(a)) return pw == 16 ? "wgrad3x3_dma_kernel<16>" : "wgrad3x3_dma_kernel<8>";
     return pw == 16 ? "wgrad3x3_kernel<16, 0>" : "wgrad3x3_kernel<8, 0>";
   }
   if (const int pw = fused22_pw(a)) {
@@ -992,12 +843,7 @@ extern "C" int stf_wgrad(const stf_wgrad_args* a, stf_stream_t stream) {
     fused_tiles(a, pw, ty, tx, nt);
     dim3 grid(splits, a->Nout / 64, c.Cs / 64);
     static const int diag = stf::ablation_env("STF_WGRAD_DIAG");
-    if (wgrad_dma(a)) {
-      const uint32_t dyb = (uint32_t)((uint64_t)c.N * c.Hd * c.Wd * a->dy_cstride * 2);
-      const uint32_t xb = (uint32_t)((uint64_t)c.N * c.Hs * c.Ws * c.src_cstride * 2);
-      if (pw == 16) hipLaunchKernelGGL((wgrad3x3_dma_kernel<16>), grid, dim3(NT), 0, s, w, ty, tx, nt, dyb, xb);
-      else hipLaunchKernelGGL((wgrad3x3_dma_kernel<8>), grid, dim3(NT), 0, s, w, ty, tx, nt, dyb, xb);
-    } else if (pw == 16 && diag == 1)
+    if (pw == 16 && diag == 1)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 1>), grid, dim3(NT), 0, s, w, ty, tx, nt);
     else if (pw == 16 && diag == 2)
       hipLaunchKernelGGL((wgrad3x3_kernel<16, 2>), grid, dim3(NT), 0, s, w, ty, tx, nt);

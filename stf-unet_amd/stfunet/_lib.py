@@ -25,6 +25,51 @@ LIB_PATH_F16 = os.environ.get("STF_LIB_F16", os.path.join(os.path.dirname(LIB_PA
 LIB_PATHS = {torch.bfloat16: LIB_PATH, torch.float16: LIB_PATH_F16}
 STORAGE_CODE = {torch.bfloat16: 0, torch.float16: 1}     # stf_storage_type()
 
+BUILD_INFO = os.path.join(_HERE, "build_info.json")     # written by __graft_entry__.build()
+_SRC_DIRS = (os.path.join(_HERE, "..", "csrc"), os.path.join(_HERE, "..", "..", "include"))
+
+
+def _sha(paths):
+    import hashlib
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def source_digest():
+    """sha256 prefix over the HIP sources, their headers and the Makefile (None if absent)."""
+    files = []
+    for d in _SRC_DIRS:
+        if os.path.isdir(d):
+            files += sorted(os.path.join(d, f) for f in os.listdir(d)
+                            if f.endswith((".hip", ".h")) or f == "Makefile")
+    return _sha(files) if files else None
+
+
+def build_info():
+    """Which build is loaded: digests of the two libraries as they are on disk, the source digest
+    recorded when they were built (build_info.json) and the digest of the sources present now --
+    src_recorded == src_now says the libraries were built from these sources."""
+    import json
+    info = {"lib": {}, "src_recorded": None, "src_now": source_digest()}
+    for dt, path in LIB_PATHS.items():
+        key = "bf16" if dt == torch.bfloat16 else "fp16"
+        info["lib"][key] = _sha([path]) if os.path.exists(path) else None
+    try:
+        with open(BUILD_INFO) as f:
+            rec = json.load(f)
+        info["src_recorded"] = rec.get("src")
+        info["lib_recorded"] = rec.get("lib")
+    except (OSError, ValueError):
+        pass
+    info["current"] = (info["src_recorded"] is not None and info["src_recorded"] == info["src_now"]
+                       and info.get("lib_recorded") == info["lib"])
+    return info
+
+
 c_uint = ctypes.c_uint
 c_int, c_void_p, c_float, c_size_t, c_int64 = (ctypes.c_int, ctypes.c_void_p, ctypes.c_float,
                                                 ctypes.c_size_t, ctypes.c_int64)

@@ -54,6 +54,7 @@ class GradAllReduce:
         # that contends with the backward for CUs and changes nothing
         self.avg = dist.get_backend(group) == "nccl" and self.world > 1
         self.prog.grad_ready_hook = self._ready
+        self.after_launch = None        # bench.py --contend: called on the joiner after each collective
         self._reset()
 
     def _reset(self):
@@ -79,6 +80,8 @@ class GradAllReduce:
                 js.wait_stream(s)
             with torch.cuda.stream(js):
                 dist.all_reduce(t, op=op, group=self.group, async_op=False)
+                if self.after_launch is not None:
+                    self.after_launch(t)
             self.works.append((None, t))
         else:
             self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t))

@@ -516,7 +516,7 @@ def _num_cus(device):
     n = _CUS.get(device)
     if n is None:
         n = torch.cuda.get_device_properties(device).multi_processor_count
-        n = _CUS[device] = int(os.environ.get("STF_SIDE_WGRAD_BLOCKS", n))    # A/B override
+        _CUS[device] = n
     return n
 
 

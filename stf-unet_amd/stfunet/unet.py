@@ -21,7 +21,6 @@ parameter to ``_UNetFunction``, an explicit schedule over NHWC bf16 buffers:
   OutConv (src/unet.py:37,56): fused with dec1's last BN+ReLU in stf_head_fwd
   backward: the mirror schedule, gradients written into one flat fp32 buffer.
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -161,18 +160,12 @@ class UNetProgram:
 
     def backward(self, S, dlogits):
         # weight gradients stay on the current stream here: a side stream (as in the STF
-        # program) measured +1 % at cfg2 but makes every concurrent kernel's duration (and
-        # so bench.py's per-kernel roofline) a shared-machine number
+        # program) measured +1.2 / -0.3..-3.8 % at cfg2 (full / one-per-CU grid, round 5) and makes
+        # every concurrent kernel's duration a shared-machine number; the variant was removed
         nhwc.ACTIVE_PACKS = self.packs
-        ws = nhwc.wgrad_side_stream(dlogits.device) if os.environ.get("STF_UNET_WGRAD_SIDE") == "1" else None
-        nhwc.WGRAD_STREAM = ws
-        nhwc.WGRAD_MAIN = torch.cuda.current_stream(dlogits.device) if ws is not None else None
         try:
             return self._backward(S, dlogits)
         finally:
-            nhwc.WGRAD_STREAM = nhwc.WGRAD_MAIN = None
-            if ws is not None:
-                nhwc.wait(torch.cuda.current_stream(dlogits.device), ws)
             nhwc.ACTIVE_PACKS = None
 
     def _forward(self, x, training, need_bwd):

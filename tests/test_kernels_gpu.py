@@ -148,6 +148,9 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     (3, 64, 64, 16, 16, 3, False, 64, 0),        # one image per group: single-image 16x16 tiles
     (16, 512, 512, 8, 8, 4, False, 512, 0),      # four 8x8 images per 8x32 tile (STF layer4)
     (8, 256, 128, 8, 8, 2, True, 320, 64),       # 8x8 four-image tiles, accumulate, slice source
+    (2, 128, 256, 37, 70, 1, False, 128, 0),     # wide kernel (128-channel slices): ragged tiles, two slices
+    (4, 256, 128, 32, 64, 2, True, 320, 64),     # wide: grouped statistics, accumulate, slice source; wide dgrad
+    (3, 64, 384, 40, 33, 3, False, 64, 0),       # wide: three slices, two chunks, one image per group
 ])
 def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
