@@ -1694,7 +1694,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t s
 // stall on LDS-DMA issue together.  Direct epilogue (16-B stores of 8 consecutive channels,
 // weight rows fetched in the permuted order of halo_body's DIRECT), BatchNorm partial statistics
 // as halo_body's non-deferred path (one row per (group, workgroup)), the slice's biases by one
-// LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad).
+// LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad, eval forward).
 #ifndef WIDE_STAGGER
 #define WIDE_STAGGER 0
 #endif
@@ -1733,7 +1733,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
   const int cnt = per + (int)(vb < rem);
   const int it0 = vb * per + min(vb, rem);
   const int S = cnt * CC;
-  const bool has_bias = DIRECT == 2 && a.bias != nullptr;
+  const bool has_bias = a.bias != nullptr;             // (eval-mode forwards run without statistics, with bias)
   const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, 0, src_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_wgt =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.wgt, 0, (uint32_t)a.Nout * a.K * 2, 0x00020000);

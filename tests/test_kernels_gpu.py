@@ -186,6 +186,21 @@ def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     assert rel(dx.dense(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("n,cin,cout,H,W", [(2, 64, 64, 37, 70), (2, 128, 256, 37, 70), (3, 256, 128, 16, 16)])
+def test_conv3x3_halo_bias_without_statistics(n, cin, cout, H, W):
+    """The eval-mode forward (bias, no BatchNorm statistics) through the halo kernels: the 64-channel
+    slices, the wide 128-channel slices (its no-statistics variant also runs the dgrads) and 16x16
+    tiles."""
+    from stfunet import nhwc
+    x = bfr(torch.randn(n, cin, H, W, device=DEV))
+    w = bfr(torch.randn(cout, cin, 3, 3, device=DEV) / (cin * 9) ** 0.5)
+    b = torch.randn(cout, device=DEV)
+    dst = nhwc.new_feat(n, H, W, cout, DEV)
+    nhwc.igemm(feat_from(x), nhwc.pack_weight(w.contiguous(), 0, cin), cout, dst, 3, 3, 1, 1, bias=b,
+               want_stats=False)
+    assert rel(dst.dense(), F.conv2d(x, w, b, padding=1)) < 1e-2
+
+
 @pytest.mark.parametrize("n,H,W,groups,dcs", [(6, 20, 36, 3, 64), (4, 64, 64, 2, 96), (2, 16, 16, 1, 64)])
 def test_conv3x3_8channel_input(n, H, W, groups, dcs):
     """The 8-channel-input 3x3 kernel (conv3x3_c8_kernel: halo of 16-B pixel rows, one
