@@ -164,6 +164,12 @@ int stf_wgrad_reduce(float* ws, int splits, int Nout, int R, int S, int Cs,
  * 1x1 convs, src/unet.py:28-37).  partial: [ceil(M/256)][C] scratch. */
 int stf_channel_sum(const void* x, int x_cstride, int M, int C, float* partial,
                     float* out, stf_stream_t stream);
+/* The same column sums taken from the BatchNorm statistics rows [tiles][2][Nout] that an
+ * stf_igemm with `stats` produced (the per-tile sums of its stored outputs): out[c] = sum over
+ * tiles of the sum half's column c0 + c, c < C.  The UNet's ConvT bias gradients come from the
+ * statistics of the dgrad that writes the concat gradient, instead of another pass over it
+ * (ABI v17). */
+int stf_stat_sums(const float* stats, int tiles, int Nout, int c0, int C, float* out, stf_stream_t stream);
 
 /* ---------------------------------------------------------------- BatchNorm2d
  * Training-mode BatchNorm2d (+ReLU) (src/unet.py:13-17; src/stf_lstm_unet.py:14-17,

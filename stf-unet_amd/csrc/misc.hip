@@ -390,6 +390,26 @@ extern "C" int stf_channel_sum(const void* x, int x_cstride, int M, int C, float
   return 0;
 }
 
+// out[c] = sum over the T rows of the statistics layout [T][2][Nout] of column c0 + c of the
+// "sum" half (fixed order, as stf_tile_sum_kernel)
+__global__ __launch_bounds__(stf::FOLD_NT) void stat_sums_kernel(const float* __restrict__ stats, int tiles, int Nout,
+                                                                 int c0, int C, float* __restrict__ out) {
+  __shared__ double red[stf::FOLD_NT];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const bool cok = c < C;
+  const double v = stf::fold16_finish(stf::fold16_partial(stats + c0, tiles, 2L * Nout, c, cok), red);
+  if (cok && (threadIdx.x >> 4) == 0) out[c] = (float)v;
+}
+
+extern "C" int stf_stat_sums(const float* stats, int tiles, int Nout, int c0, int C, float* out,
+                             stf_stream_t stream) {
+  if (!stats || !out || tiles < 1 || C < 1 || c0 < 0 || c0 + C > Nout) return STF_EINVAL;
+  hipLaunchKernelGGL(stat_sums_kernel, dim3((C + 15) / 16), dim3(stf::FOLD_NT), 0, (hipStream_t)stream, stats, tiles,
+                     Nout, c0, C, out);
+  STF_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" const char* stf_error_string(int code) {
   if (code == STF_EINVAL) return "stfunet: invalid argument (shape/alignment constraint violated)";
   return hipGetErrorString((hipError_t)code);

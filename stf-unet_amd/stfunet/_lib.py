@@ -153,6 +153,7 @@ _SIGS = {
     "stf_lstm_coop_error": (c_int, [P, c_int, c_int, P, P]),
     "stf_bilinear_ac_fwd": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P]),
     "stf_bilinear_ac_bwd": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, P]),
+    "stf_stat_sums": (c_int, [P, c_int, c_int, c_int, c_int, P, P]),
     "stf_bilinear_ac_bwd_tsum": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int64, c_int64, c_int,
                                          c_int, P]),
     "stf_eval_counts_sm": (c_int, [P, P, P, c_int, c_int, c_int64, c_int64, P, P, P]),

@@ -422,17 +422,19 @@ def _plan_tag(a, fn, key, flops):
     call("stf_plan_tag", _kernel_name(fn, key, a).encode(), float(flops))
 
 
-def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None, cache=True):
+def conv_dgrad(dy: Feat, w, dx: Feat, R, S, stride, pad, accumulate=False, bnr=None, cache=True, want_stats=False):
     """Conv2d input gradient: stride 1 runs as a forward gather over flipped taps
     (pack mode 5, pad' = R-1-pad); strided convs use the transposed gather.
     ``accumulate``: dx += gradient (residual / multi-consumer tensors).
     ``bnr`` = (y, BNState, relu): dx feeds the backward of act(BN(y)); returns the
     fused partial sums and tiles for bn_backward_fused.  ``cache=False``: ``w`` is a per-call
-    temporary (pack_weight)."""
+    temporary (pack_weight).  ``want_stats``: also the per-tile (sum, sum of squares) rows of the
+    stored dx (stride-1 only; stat_sums folds columns of them)."""
     groups = bnr[1].groups if bnr is not None else 1
     if stride == 1 and 2 * pad == R - 1 and R == S:
         return igemm(dy, pack_weight(w, 5, cache=cache), dx.C, dx, R, S, 1, R - 1 - pad, accumulate=accumulate,
-                     bnr=bnr, groups=groups)
+                     bnr=bnr, groups=groups, want_stats=want_stats)
+    assert not want_stats
     return igemm(dy, pack_weight(w, 1, cache=cache), dx.C, dx, R, S, stride, pad, transposed=True,
                  accumulate=accumulate,
                  bnr=bnr, groups=groups)
@@ -553,6 +555,12 @@ def _wgrad(dy: Feat, x: Feat, R, S, stride, pad, out, grid_blocks=0):
         t.end(ev, name, 2.0 * dy.M * dy.C * R * S * x.C,
               f"wgrad M={dy.M} N={dy.C} K={R * S * x.C} {R}x{S}/s{stride} splits={splits}")
     call("stf_wgrad_reduce", ws.data_ptr(), splits, dy.C, R, S, x.C, out.data_ptr(), stream())
+
+
+def stat_sums(stats, tiles, nout, c0, C, out):
+    """out[c] = sum of column c0 + c of the sum half of igemm statistics rows [tiles][2][nout]."""
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == C
+    call("stf_stat_sums", _p(stats), tiles, nout, c0, C, _p(out), stream())
 
 
 def channel_sum(x: Feat, out):

@@ -57,9 +57,10 @@ class DoubleConvProgram:
         with nhwc.timed_block(f"{self.name}.fwd"):
             return self._forward(src, training, need_bwd, out, pooled)
 
-    def backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None):
+    def backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None,
+                 dsrc_stats=False):
         with nhwc.timed_block(f"{self.name}.bwd"):
-            return self._backward(s, grads, need_dsrc, dz, dpool, dy2)
+            return self._backward(s, grads, need_dsrc, dz, dpool, dy2, dsrc_stats)
 
     def _forward(self, src: Feat, training, need_bwd, out: Feat = None, pooled: Feat = None):
         conv1, bn1, conv2, bn2 = self.blk[0], self.blk[1], self.blk[3], self.blk[4]
@@ -81,9 +82,12 @@ class DoubleConvProgram:
         s.y1, s.a1, s.y2 = y1, a1, y2
         return s if need_bwd else None
 
-    def _backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None):
+    def _backward(self, s, grads, need_dsrc, dz: Feat = None, dpool: Feat = None, dy2: Feat = None,
+                  dsrc_stats=False):
         """Either (dz and/or dpool) w.r.t. the block output, or dy2 (grad w.r.t.
-        the raw second conv output, when the BN backward was fused upstream)."""
+        the raw second conv output, when the BN backward was fused upstream).  ``dsrc_stats``:
+        return (dsrc, statistics rows, tiles) -- the per-tile column sums of the stored input
+        gradient (a decoder block's concat gradient: the up-conv's bias gradient, no extra pass)."""
         conv1, bn1, conv2, bn2 = self.blk[0], self.blk[1], self.blk[3], self.blk[4]
         gv = grads.grad_view
         if dy2 is None:
@@ -108,8 +112,8 @@ class DoubleConvProgram:
             wp = nhwc.memset0(nhwc.empty((self.cout, s.src.C, 3, 3), torch.float32, w1.device))
             nhwc.copy_rows(w1.detach(), cin * 9, wp, s.src.C * 9, self.cout, cin * 9)
             w1 = wp
-        nhwc.conv_dgrad(dy1, w1, dsrc, 3, 3, 1, 1, cache=w1 is conv1.weight)
-        return dsrc
+        st, tiles = nhwc.conv_dgrad(dy1, w1, dsrc, 3, 3, 1, 1, cache=w1 is conv1.weight, want_stats=dsrc_stats)
+        return (dsrc, st, tiles) if dsrc_stats else dsrc
 
     def _wgrad_conv1(self, dy1, src, out):
         cin = self.blk[0].in_channels
@@ -239,24 +243,27 @@ class UNetProgram:
         dec1 = self.decs[3]
         dy2 = nhwc.bn_backward_from_partial(g, s.y2, s.bn2, dec1.blk[4], bnp, tiles, gv(dec1.blk[4].weight),
                                             gv(dec1.blk[4].bias), gv(dec1.blk[3].bias))
-        dcat = dec1.backward(s, self.flat, True, dy2=dy2)
+        # the concat gradient of each decoder block comes with the per-tile column sums of what its
+        # dgrad stored (statistics epilogue): the up-conv's bias gradient is their up-half fold
+        dcat, cst, ctiles = dec1.backward(s, self.flat, True, dy2=dy2, dsrc_stats=True)
         self._done(dec1.blk)
         dcats = [None] * 4
-        dcats[0] = dcat
+        dcats[0] = (dcat, cst, ctiles)
         # decoder levels 2..4 and the up-convs, deepest last
         for i in (3, 2, 1, 0):                       # index into self.ups / S.dec_in (up1 is i=3)
             up = self.ups[i]
-            dcat = dcats[3 - i]
+            dcat, cst, ctiles = dcats[3 - i]
+            dcats[3 - i] = dcat
             Clo = self.decs[i].cout
             dup = dcat.slice(0, Clo)
             src = S.dec_in[i]
             nhwc.wgrad(src, dup, 2, 2, 2, 0, gv(up.weight))
-            nhwc.channel_sum(dup, gv(up.bias))
+            nhwc.stat_sums(cst, ctiles, dcat.C, 0, Clo, gv(up.bias))       # (= channel_sum(dup))
             dsrc = new_feat(src.N, src.H, src.W, src.C, dev)
             nhwc.igemm(dup, nhwc.pack_weight(up.weight, 3), src.C, dsrc, 2, 2, 2, 0)
             self._done(up)
             if i > 0:
-                dcats[4 - i] = self.decs[i - 1].backward(S.dec[i - 1], self.flat, True, dz=dsrc)
+                dcats[4 - i] = self.decs[i - 1].backward(S.dec[i - 1], self.flat, True, dz=dsrc, dsrc_stats=True)
                 self._done(self.decs[i - 1].blk)
             else:
                 d_b = dsrc
