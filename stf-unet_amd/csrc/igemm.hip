@@ -1711,17 +1711,23 @@ constexpr int G0BYTES = G1T * BN * 64;                  // 40960 B
 constexpr int WOFF = 2 * HSTAGE;                        // 81920: G0, then G1 at WOFF + G0BYTES
 constexpr int BOFF = WOFF + 9 * BN * 64;                // 155648: the slice's 128 biases (1 KiB DMA target)
 constexpr int ROFF = BOFF + 1024;                       // 156672: running statistics partials [2][128] fp32
-constexpr int LDS = ROFF + 1024;                        // 157696
+constexpr int AOFF = ROFF + 1024;                       // 157696: BNR -- the item's BatchNorm affine
+                                                        // [scale | shift | mean | invstd][128] fp32, 1 KiB DMA slot each
+constexpr int LDS = AOFF + 4096;                        // 161792
 constexpr int TM = 4, TN = 8, NST = 2 * TN;             // 16 epilogue stores per lane
 static_assert(HIN * RPI >= HR && HIN % NW == 0 && G1T * BN % (RPI * NW) == 0 && (9 - G1T) * BN % (RPI * NW) == 0,
               "wide halo geometry");
 static_assert(NW * 2 * BN * 4 <= (9 - G1T) * BN * 64, "statistics scratch in the G1 weight buffer");
 }
 
-template <int DIRECT>
+// BNR (with DIRECT 1): the dgrad's output dz feeds the backward of ReLU(BN(y)); the epilogue also
+// reduces the BatchNorm-backward partials (sum g, sum g*xhat), g = dz * [y*scale+shift > 0], as
+// halo_body's BNR (same partial rows), y read per 32-channel block into registers
+template <int DIRECT, bool BNR = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t src_bytes, int TY, int TX, int per,
                                                               int rem) {
   using namespace wide;
+  static_assert(!BNR || DIRECT == 1, "BNR: a dgrad, no statistics");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1783,6 +1789,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_wgt, (lds_ptr)(wb + (wave * GPW + i) * RPI * 64), 16, off, 0, 0, 0);
     }
   };
+  // BNR, wave 0, first chunk of an item: the item's (group, slice) affine, four 512-B arrays, each by
+  // one DMA instruction into its own 1 KiB slot (lanes 32..63 out of range write zeros after it)
+  auto issue_aff = [&](int s) {
+    const int item = it0 + s / CC;
+    const int nt = item / ntiles, img = (item - nt * ntiles) / tpi;
+    const uint32_t nbytes = (uint32_t)(a.M / a.Mg) * a.Nout * 4;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const uint32_t off = ln < BN / 4 ? (uint32_t)(((img / ipg) * a.Nout + nt * BN + ln * 4) * 4) : BAD;
+    const float* arr[4] = {a.bnr_scale, a.bnr_shift, a.bnr_mean, a.bnr_invstd};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(__builtin_amdgcn_make_buffer_rsrc((void*)arr[k], 0, nbytes, 0x00020000),
+                                               (lds_ptr)(smem + AOFF + k * 1024), 16, off, 0, 0, 0);
+  };
   // wave 0, first chunk of an item: the slice's 128 biases (lanes 0..31 x 16 B) into BOFF
   auto issue_bias = [&](int s) {
     const int nt = (it0 + s / CC) / ntiles;
@@ -1815,8 +1836,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
 
   // BatchNorm partial statistics rows [groups][gridDim][2][Nout], as halo_body (non-deferred): thread
   // tid < 256 owns (sum | sum of squares, channel) tid of the current (group, slice) key, its running
-  // value in LDS (ROFF) and its row addresses recomputed when used (registers go to the accumulators)
-  float* const sbuf = DIRECT == 2 ? a.stats : nullptr;
+  // value in LDS (ROFF) and its row addresses recomputed when used (registers go to the accumulators).
+  // BNR: the same rows hold (sum g, sum g*xhat)
+  float* const sbuf = BNR ? a.bnr_part : (DIRECT == 2 ? a.stats : nullptr);
   float* const runl = reinterpret_cast<float*>(smem + ROFF);
   const int groups = a.M / a.Mg;
   auto srow_ptr = [&](int key) {                        // (group, slice) key -> this thread's element
@@ -1875,6 +1897,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
       auto issue_point = [&]() {
         if (g == 0) {
           if (has_bias && cc == 0 && wave == 0) issue_bias(s);
+          if (BNR && cc == 0 && wave == 0) issue_aff(s);
           issue_w(s, std::integral_constant<int, 1>());
           issue_halo(s + 1);
         } else {
@@ -1938,8 +1961,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
         mq[i] = (y < a.Hd && x < a.Wd) ? (img * a.Hd + y) * a.Wd + x : -1;
       }
       float res[4] = {0.f, 0.f, 0.f, 0.f};
+      const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)a.bnr_y, 0, BNR ? (uint32_t)((size_t)a.M * a.bnr_ycs * 2) : 0u, 0x00020000);
+      // BNR: y of the lane's 8 channels of each pixel, one 32-channel block ahead (the MFMA operand
+      // registers are free in the epilogue)
+      uint4 yq[2][TM];
+      auto load_y = [&](int h) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const uint32_t yo = mq[i] >= 0 ? (uint32_t)(((size_t)mq[i] * a.bnr_ycs + nt * BN + h * 32 + ko * 8) * 2) : BAD;
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_y, yo, 0, 0);
+          yq[h & 1][i] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+      };
+      if constexpr (BNR) load_y(0);
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
+        if constexpr (BNR)
+          if (h < 3) load_y(h + 1);
         float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         if (has_bias) {
           const float4 lo = *reinterpret_cast<const float4*>(smem + BOFF + (h * 32 + ko * 8) * 4);
@@ -1977,8 +2016,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
 #pragma unroll
             for (int e = 0; e < 8; ++e) { v[e] += w * gq[e]; v[8 + e] += w * gq[e] * gq[e]; }
           }
+          if constexpr (BNR) {
+            // g = dz * [y*scale+shift > 0] (valid pixels); v: sum g, then sum g*y (-> g*xhat below)
+            float gq[8], yv[8];
+            unpack8(u, gq);
+            unpack8(yq[h & 1][i], yv);
+            const float* af = reinterpret_cast<const float*>(smem + AOFF) + h * 32 + ko * 8;
+            const bool valid = mq[i] >= 0, norelu = !a.bnr_relu;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const bool keep = valid & (norelu | (yv[e] * af[e] + af[256 + e] > 0.f));
+              const float gg = keep ? gq[e] : 0.f;
+              v[e] += gg;
+              v[8 + e] += gg * yv[e];
+            }
+          }
         }
-        if constexpr (DIRECT == 2) res[h] = row16_reduce_scatter(v, fo);
+        if constexpr (BNR) {
+          const float* af = reinterpret_cast<const float*>(smem + AOFF) + h * 32 + ko * 8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 + e] = af[768 + e] * (v[8 + e] - af[512 + e] * v[e]);
+        }
+        if constexpr (DIRECT == 2 || BNR) res[h] = row16_reduce_scatter(v, fo);
       }
       epi = true;
       if (sbuf) {
@@ -2244,12 +2303,15 @@ int halo_grid(const stf_igemm_args* a, int ix);
 void halo_tiles(const stf_conv_geom& c, int& ty, int& tx);
 
 // the wide halo kernel (conv3x3_wide_kernel: 128-channel output slices) for 3x3 layers with >= 128
-// output channels and W >= 32, forward and plain dgrad (not the BN-backward-fused dgrad);
-// STF_HALO_WIDE=0: the 64-channel halo kernel (A/B)
+// output channels and W >= 32, forward, plain dgrad and BN-backward-fused dgrad (STF_WIDE_BNR=0: that one
+// on the 64-channel kernel, A/B); STF_HALO_WIDE=0: the 64-channel halo kernel (A/B)
+bool bnr_fused(const stf_igemm_args* a, char k);
 bool halo_wide(const stf_igemm_args* a) {
   static const int on = stf::ab_switch("STF_HALO_WIDE", 1);
+  static const int wbnr = stf::ab_switch("STF_WIDE_BNR", 1);
   const stf_conv_geom& c = a->g;
-  return on && !a->bnr && !a->lstm && !a->scatter2x2 && !c.transposed && halo_direct(a) && a->Nout % 128 == 0 &&
+  if (a->bnr && !(wbnr && bnr_fused(a, 'H'))) return false;
+  return on && !a->lstm && !a->scatter2x2 && !c.transposed && halo_direct(a) && a->Nout % 128 == 0 &&
          c.Wd >= 32 && c.Cs % 32 == 0 && halo_ix(a, a->stats != nullptr) == 1;
 }
 
@@ -2536,7 +2598,7 @@ extern "C" const char* stf_igemm_kernel_name(const stf_igemm_args* a) {
       if (halo8(a))
         snprintf(buf, sizeof buf, "conv3x3_halo4_kernel<0>");
       else if (halo_wide(a))
-        snprintf(buf, sizeof buf, "conv3x3_wide_kernel<%d>", a->stats ? 2 : 1);
+        snprintf(buf, sizeof buf, "conv3x3_wide_kernel<%d, %s>", a->stats ? 2 : 1, a->bnr ? "true" : "false");
       else if (halo_ix(a, a->stats != nullptr) > 1)
         snprintf(buf, sizeof buf, "conv3x3_halo2_kernel<%d, %s, %s>", halo_direct(a) ? (a->stats ? 2 : 1) : 0,
                  bnr_fused(a, k) ? "true" : "false", halo_defer(a) ? "true" : "false");
@@ -2672,6 +2734,8 @@ static int igemm_launch(const stf_igemm_args* a, stf_stream_t stream) {
     } while (0)
     if (ix == 1 && halo_wide(a)) {
       if (d == 2) hipLaunchKernelGGL((conv3x3_wide_kernel<2>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per, rem);
+      else if (a->bnr) hipLaunchKernelGGL((conv3x3_wide_kernel<1, true>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx,
+                                          per, rem);
       else hipLaunchKernelGGL((conv3x3_wide_kernel<1>), dim3(grid), dim3(512), 0, s, g, src_bytes, ty, tx, per, rem);
     } else if (ix == 4) {
       hipLaunchKernelGGL((conv3x3_halo4_kernel<0>), dim3(grid), dim3(256), 0, s, g, src_bytes, ty, tx, per, rem);

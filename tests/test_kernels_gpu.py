@@ -267,6 +267,9 @@ def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
     (2, 64, 64, 64, 64, 1, False, True),      # plain BN (no ReLU), accumulate
     (6, 256, 128, 8, 8, 2, True, False),      # linear kernel (6 images: no 4-image halo tiles): separate reduce
     (8, 256, 128, 8, 8, 2, True, False),      # 8x8 four-image halo tiles: separate reduce
+    (2, 128, 64, 40, 72, 2, True, False),     # wide kernel (128-channel slice), ragged, one image per group
+    (4, 256, 64, 48, 40, 2, True, False),     # wide kernel, two slices x two groups per workgroup run
+    (2, 128, 128, 64, 64, 1, False, True),    # wide kernel, plain BN, accumulate
 ])
 def test_dgrad_fused_bn_backward_reduce(n, cin, cout, H, W, groups, relu, acc):
     """conv_dgrad with ``bnr``: dz identical to the plain dgrad, and the fused partial
