@@ -1695,6 +1695,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t s
 // weight rows fetched in the permuted order of halo_body's DIRECT), BatchNorm partial statistics
 // as halo_body's non-deferred path (one row per (group, workgroup)), the slice's biases by one
 // LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad, eval forward).
+#ifndef WIDE_ABL          // timing-only ablations (results wrong): 1 = half the B-fragment LDS reads,
+#define WIDE_ABL 0        // 2 = no LDS-DMA fills after the first stage (3: no weight fills, 4: no halo fills,
+                          // 5: every item's halo from tiles 0 / 1 (L2 hits))
+#endif
 #ifndef WIDE_STAGGER
 #define WIDE_STAGGER 0
 #endif
@@ -1752,7 +1756,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
   auto issue_halo = [&](int s) {
     const bool live = s < S;
     const int item = it0 + (live ? s / CC : 0), cc = live ? s % CC : 0;
-    const int tile = item % ntiles;
+    const int tile = WIDE_ABL == 5 ? item % 2 : item % ntiles;
     const int img = tile / tpi, t2 = tile - img * tpi, ty = t2 / TX, tx = t2 - ty * TX;
     const int y0 = ty * PH - 1, x0 = tx * PW - 1;
     char* st = smem + (s & 1) * HSTAGE;
@@ -1895,13 +1899,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       auto issue_point = [&]() {
+        if (WIDE_ABL == 2 && s >= 1) return;
+        const bool wl = !(WIDE_ABL == 3 && s >= 1), hl = !(WIDE_ABL == 4 && s >= 1);
         if (g == 0) {
           if (has_bias && cc == 0 && wave == 0) issue_bias(s);
           if (BNR && cc == 0 && wave == 0) issue_aff(s);
-          issue_w(s, std::integral_constant<int, 1>());
-          issue_halo(s + 1);
+          if (wl) issue_w(s, std::integral_constant<int, 1>());
+          if (hl) issue_halo(s + 1);
         } else {
-          issue_w(s + 1, std::integral_constant<int, 0>());
+          if (wl) issue_w(s + 1, std::integral_constant<int, 0>());
         }
       };
       if (WIDE_STAGGER == 0 || wave < NW / 2) issue_point();   // (stagger: waves 4..7 after their first MFMA block)
@@ -1910,7 +1916,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
       // MFMAs run
       if (g == 0) rdA(0, 0, ph);
       rdB(t0, 0);
-      rdB(t0, 1);
+      if (WIDE_ABL == 1) { wf[4] = wf[0]; wf[5] = wf[1]; wf[6] = wf[2]; wf[7] = wf[3]; }
+      else rdB(t0, 1);
 #pragma unroll
       for (int t = t0; t < t1; ++t) {
         const int b = t & 1;
@@ -1939,7 +1946,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wide_kernel(Geo a, uint32_t sr
         for (int jj = 4; jj < 8; ++jj)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[i][jj] = mfma16x16x32(wf[jj], xf[b][i], acc[i][jj]);
-        if (nB) rdB(t + 1, 1);
+        if (nB) {
+          if (WIDE_ABL == 1) { wf[4] = wf[0]; wf[5] = wf[1]; wf[6] = wf[2]; wf[7] = wf[3]; }
+          else rdB(t + 1, 1);
+        }
       }
     }
     if (++cc < CC) continue;
