@@ -569,6 +569,8 @@ def _build_record():
     """Which build ran: the loaded libraries' digests and the source digest they were built from
     (__graft_entry__.build() records it next to them)."""
     from stfunet import _lib
+    if not hasattr(_lib, "build_info"):          # (an older package under STF_PKG_ROOT)
+        return None
     i = _lib.build_info()
     return {"src": i["src_recorded"], "src_now": i["src_now"], "lib": i["lib"], "current": i["current"]}
 
