@@ -367,6 +367,25 @@ class _BN:
             self.bn.bias.uniform_(-0.5, 0.5)
 
 
+@pytest.mark.parametrize("n,C,H,W,groups", [(4, 64, 20, 12, 2), (2, 128, 16, 16, 1), (6, 256, 6, 10, 3)])
+def test_bn_act_pool_bitwise(n, C, H, W, groups):
+    """The pooled BN apply (BN + ReLU + Down's 2x2 max pool in one pass): its full-size output equals
+    the un-pooled apply bit for bit, and its pooled output is exactly the 2x2 max of that output
+    (grouped statistics, a channel slice of a wider source and destination)."""
+    from stfunet import nhwc
+    y = feat_from(torch.randn(n, C, H, W, device=DEV) * 2 + 0.3, cs=C + 64, off=32)
+    st = nhwc.BNState(C, DEV, n * H * W, groups)
+    st.scale.copy_(torch.randn(groups, C, device=DEV))
+    st.shift.copy_(torch.randn(groups, C, device=DEV) * 0.5)
+    ref = nhwc.zeros_feat(n, H, W, C, DEV)
+    nhwc.bn_act(y, st, ref)
+    out = nhwc.zeros_feat(n, H, W, 2 * C, DEV).slice(C, C)
+    pooled = nhwc.new_feat(n, H // 2, W // 2, C, DEV)
+    nhwc.bn_act(y, st, out, pooled=pooled)
+    assert torch.equal(out.dense(), ref.dense())
+    assert torch.equal(pooled.dense(), F.max_pool2d(ref.dense(), 2))
+
+
 @pytest.mark.parametrize("pool,C", [(False, 64), (True, 64), (True, 128), (True, 512)])
 def test_bn_forward_backward(pool, C):
     from stfunet import nhwc
