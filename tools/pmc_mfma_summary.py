@@ -120,11 +120,17 @@ def main():
            "fit_clock_ghz": round(fit_clock, 3), "fit_overread_cycles_per_dispatch": round(fit_c0),
            "kernels": kernels}
     if a.unet_layers:
-        halo = [e for e in ev if e["name"].startswith("conv3x3_halo_kernel<16, 32, 8, 2, 0, 2, false")]
+        # (forward convs with BN statistics: the 64-channel halo kernel and, at >= 128 output
+        # channels, the wide kernel since round 6)
+        halo = [e for e in ev if e["name"].startswith(("conv3x3_halo_kernel<16, 32, 8, 2, 0, 2, false",
+                                                       "conv3x3_wide_kernel<2"))]
+        # per step: the 15 forward convs, then (since round 6) the 4 dgrads that write the concat
+        # gradients with statistics rows (the ConvT bias gradients, stf_stat_sums) in the backward
         n = len(UNET_FWD_HALO)
+        per_step = n + 4 if len(halo) % (n + 4) == 0 else n
         layers = defaultdict(list)
-        for i, e in enumerate(halo[(len(halo) // n - 1) * n:]):   # the last profiled step
-            layers[UNET_FWD_HALO[i % n]].append(derive(e) | {"us": e["dur_ns"] / 1e3})
+        for i, e in enumerate(halo[len(halo) - per_step:][:n]):   # the last profiled step's forward
+            layers[UNET_FWD_HALO[i]].append(derive(e) | {"us": e["dur_ns"] / 1e3})
         res["forward_halo_layers_last_step"] = {
             k: {"us": round(v[0]["us"], 1), "clock_ghz": round(v[0]["clock_ghz"], 3),
                 "mfma_busy_util": round(v[0]["mfma_util"], 4),
