@@ -8,5 +8,5 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 500 rocprofv3 --pmc $c --kernel-trace -d "$GRAFT_REPO_ROOT/$out/$c" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-kernel-timer "$@" > "$GRAFT_REPO_ROOT/$out/$c.log" 2>&1
+    python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-kernel-timer --no-dice "$@" > "$GRAFT_REPO_ROOT/$out/$c.log" 2>&1
 done
