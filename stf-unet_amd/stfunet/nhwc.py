@@ -40,6 +40,8 @@ class KernelTimer:
 
     def __init__(self, only=None, log=False):
         self.rec = {}
+        self.rec_main = {}   # the same, launches on the stream current at construction only
+        self.main_stream = torch.cuda.current_stream().stream_id if torch.cuda.is_available() else None
         self.only = only
         self.tags = {}       # tag -> {"conv": [(ev0, ev1, flops)], "block": [(ev0, ev1)]}
         self.log = [] if log else None     # per launch: (shape, kernel, ev0, ev1, stream) in issue order
@@ -88,15 +90,19 @@ class KernelTimer:
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record(torch.cuda.current_stream())
         self.rec.setdefault(family, []).append((ev0, ev1, flops))
+        if torch.cuda.current_stream().stream_id == self.main_stream:
+            self.rec_main.setdefault(family, []).append((ev0, ev1, flops))
         if self.log is not None:
             self.log.append((desc, family, ev0, ev1, torch.cuda.current_stream().stream_id, flops))
         if TIMER_TAG is not None:
             self.tags.setdefault(TIMER_TAG, {"conv": [], "block": []})["conv"].append((ev0, ev1, flops))
 
-    def summary(self):
+    def summary(self, main_only=False):
+        """Per device kernel: launches, summed ms, FLOPs, average us, TF/s (``main_only``: the
+        launches on the constructing stream -- the step's compute stream -- only)."""
         torch.cuda.synchronize()
         out = {}
-        for fam, items in self.rec.items():
+        for fam, items in (self.rec_main if main_only else self.rec).items():
             ms = sum(a.elapsed_time(b) for a, b, _ in items)
             fl = sum(f for _, _, f in items)
             out[fam] = dict(launches=len(items), ms=ms, flops=fl,
