@@ -1689,12 +1689,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo4_kernel(Geo a, uint32_t s
 // (the weights are L2-resident: 4-5 taps of MFMAs cover their fill; the halo has a whole stage).
 // Every wave issues the same count at every point (4 + 5 and 5 DMA instructions, past the last
 // stage with all lanes out of range), so the waits are fixed vmcnt values.  The first tap of G1
-// reads its halo fragments before the P1 barrier.  Waves 4..7 (the SIMD partners of 0..3)
-// issue their share after the first tap's first MFMA block, so the two waves of a SIMD do not
-// stall on LDS-DMA issue together.  Direct epilogue (16-B stores of 8 consecutive channels,
-// weight rows fetched in the permuted order of halo_body's DIRECT), BatchNorm partial statistics
-// as halo_body's non-deferred path (one row per (group, workgroup)), the slice's biases by one
-// LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad, eval forward).
+// reads its halo fragments before the P1 barrier.  Every wave issues its fills in one burst right
+// after each barrier (measured against the alternatives: waves 4..7 after their first MFMA block
+// -- WIDE_STAGGER, spills; the pieces spread through the taps; one wave per SIMD issuing for
+// both -- all slower).  Direct epilogue (16-B stores of 8 consecutive
+// channels, weight rows fetched in the permuted order of halo_body's DIRECT), BatchNorm partial
+// statistics as halo_body's non-deferred path (one row per (group, workgroup)), the slice's biases
+// by one LDS-DMA of wave 0 per item.  DIRECT: 2 = forward with statistics, 1 = no statistics (dgrad,
+// eval forward); BNR (with 1): the BN-backward-fused dgrad.
 #ifndef WIDE_ABL          // timing-only ablations (results wrong): 1 = half the B-fragment LDS reads,
 #define WIDE_ABL 0        // 2 = no LDS-DMA fills after the first stage (3: no weight fills, 4: no halo fills,
                           // 5: every item's halo from tiles 0 / 1 (L2 hits))
