@@ -2406,6 +2406,8 @@ char choose(const stf_igemm_args* a, bool dma_ok) {
   if (f == 'H' && halo_ok) return 'H';
   // auto: the halo kernel for full-size 3x3 layers ('L' = auto over the linear kernels only)
   if (f == '0' && halo_ok && (c.Wd >= 32 || (c.Wd >= HALO_MIN_W && a->Nout <= 256))) return 'H';
+  // 16 x 16 layers with more output channels (UNet's bottleneck): the two-image halo tiles
+  if (f == '0' && halo_ok && a->Nout > 256 && halo_ix(a, a->stats != nullptr) == 2) return 'H';
   if (f == '0' && halo_ok && halo8(a)) return 'H';
   if (f != '0' && f != 'H' && f != 'L') {
     if (f == 'A' || f == 'E') return (f == 'E' && !(a->Nout <= 64 && !a->lstm)) ? 'A' : f;
@@ -2522,7 +2524,10 @@ int halo_ix(const stf_igemm_args* a, bool with_stats) {
   static const int mode = stf::ab_switch("STF_HALO2", 1);
   const stf_conv_geom& c = a->g;
   if (halo8(a)) return 4;
-  if (mode == 0 || (mode == 1 && !with_stats)) return 1;
+  // (mode 1: two images per tile for the forward convs with statistics, and for every conv with more
+  // than 256 output channels -- the UNet bottleneck, whose dgrads run 4-22 % faster on them than on
+  // single-image tiles or the linear kernels, tools/bench_layers.py)
+  if (mode == 0 || (mode == 1 && !with_stats && a->Nout <= 256)) return 1;
   if (c.Hd != 16 || c.Wd != 16 || c.N % 2) return 1;
   const long M = (long)c.N * c.Hd * c.Wd;
   const long Mg = a->group_rows > 0 ? a->group_rows : M;

@@ -151,6 +151,7 @@ def test_wgrad_fused_3x3(n, cin, cout, H, W, xcs, xoff, dycs):
     (2, 128, 256, 37, 70, 1, False, 128, 0),     # wide kernel (128-channel slices): ragged tiles, two slices
     (4, 256, 128, 32, 64, 2, True, 320, 64),     # wide: grouped statistics, accumulate, slice source; wide dgrad
     (3, 64, 384, 40, 33, 3, False, 64, 0),       # wide: three slices, two chunks, one image per group
+    (4, 1024, 512, 16, 16, 2, False, 1024, 0),   # UNet bottleneck (> 256 outputs at 16x16): two-image tiles, dgrad too
 ])
 def test_conv3x3_halo(n, cin, cout, H, W, groups, acc, xcs, xoff):
     """3x3/s1/p1 conv through the halo kernel (auto for W >= 64): output, grouped
@@ -270,6 +271,7 @@ def test_conv_splitk(n, cin, cout, H, W, R, groups, acc):
     (2, 128, 64, 40, 72, 2, True, False),     # wide kernel (128-channel slice), ragged, one image per group
     (4, 256, 64, 48, 40, 2, True, False),     # wide kernel, two slices x two groups per workgroup run
     (2, 128, 128, 64, 64, 1, False, True),    # wide kernel, plain BN, accumulate
+    (4, 512, 1024, 16, 16, 2, True, False),   # > 256 outputs at 16x16: two-image halo tiles (UNet bottleneck)
 ])
 def test_dgrad_fused_bn_backward_reduce(n, cin, cout, H, W, groups, relu, acc):
     """conv_dgrad with ``bnr``: dz identical to the plain dgrad, and the fused partial
