@@ -62,10 +62,12 @@ def _f16():
 
 @pytest.mark.parametrize("cin,cout,H,W,stride,R", [(64, 64, 32, 40, 1, 3), (128, 64, 16, 16, 1, 3),
                                                     (64, 128, 16, 18, 2, 3), (256, 512, 8, 8, 1, 3),
-                                                    (64, 256, 16, 16, 1, 1)])
+                                                    (64, 256, 16, 16, 1, 1), (128, 128, 32, 40, 1, 3),
+                                                    (512, 512, 16, 16, 1, 3)])
 def test_conv_fwd_dgrad_wgrad_fp16(cin, cout, H, W, stride, R):
     """Forward (+ BN statistics), input gradient and weight gradient on fp16 operands:
-    halo kernel (3x3/s1, W >= 32), linear kernels, strided gather, 1x1."""
+    halo kernel (3x3/s1, W >= 32), the wide 128-channel-slice kernel, two-image 16x16 tiles for > 256
+    outputs, linear kernels, strided gather, 1x1."""
     from stfunet import nhwc
     pad = R // 2
     x = hr(torch.randn(2, cin, H, W, device=DEV))
